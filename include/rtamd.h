@@ -1,0 +1,172 @@
+/* rtamd.h -- C ABI of the MI355X-native primary-ray renderer.
+ *
+ * Drop-in boundary for the per-pixel intersection hot path of
+ * iMacsimus/Triangles-SDF-CPU-RayTracing (reference @ 2025-07-04). The reference
+ * has no FFI for this path other than the per-node ISPC exports
+ * (src/ray_pack.ispc:220,242,290); a per-node call across a device boundary is
+ * infeasible, so the boundary sits at FRAME granularity, mirroring
+ *     float Renderer::draw(const IScene&, FrameBuffer&, const Camera&,
+ *                          const float4x4 projInv) const       (src/raytracing.hpp:109-110)
+ * and, for ray-level checks,
+ *     virtual HitInfo IScene::intersect(rayPos, rayDir, tNear, tFar) const
+ *                                                           (src/raytracing.hpp:77-79)
+ *
+ * Plain C types only: pointers + sizes, no torch, no HIP types in signatures
+ * (streams are passed as void*). Every entry point returns 0 on success or a
+ * negative RT_E* code; rt_last_error() gives a message (thread-local).
+ * Nothing throws across the ABI.
+ */
+#ifndef RTAMD_H
+#define RTAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTAMD_ABI_VERSION 1
+
+enum rt_status {
+  RT_OK = 0,
+  RT_E_INVALID = -1,   /* bad argument */
+  RT_E_IO = -2,        /* file missing / truncated */
+  RT_E_DEVICE = -3,    /* HIP runtime error (no GPU, OOM, launch failure) */
+  RT_E_STATE = -4      /* wrong scene kind for the call */
+};
+
+/* ShadingMode, same order as the reference enum (src/raytracing.hpp:99). */
+enum rt_shading_mode { RT_SHADING_NORMAL = 0, RT_SHADING_LAMBERT = 1, RT_SHADING_COLOR = 2 };
+
+enum rt_scene_kind { RT_SCENE_MESH = 1, RT_SCENE_GRID = 2, RT_SCENE_OCTREE = 3 };
+
+/* rt_render flags */
+#define RT_FLAG_CLEAR 1u /* treat the framebuffer as FrameBuffer::clear()ed (color=0, t=+inf;
+                            src/raytracing.hpp:16-19) and write every pixel: clear+draw fused.
+                            Without it, t is read as tPrev and color/t are written only on hit
+                            (src/raytracing.cpp:89-94). */
+
+typedef struct rt_scene rt_scene; /* opaque: owns the device copy of one scene on one GPU */
+
+/* Per-frame parameters. Matrices are column-major float[16] (LiteMath float4x4
+ * m_col[4] layout: element (r,c) at [c*4 + r]).
+ *   view_inv = inverse4x4(camera.lookAtMatrix())           (src/raytracing.cpp:73-75)
+ *   proj_inv = inverse4x4(perspectiveMatrix(45, W/H, 0.01, 100)) (src/main.cpp:198-201)
+ * rtamd_camera() computes both exactly as the reference does. */
+typedef struct rt_render_params {
+  float camera_pos[3];       /* Camera::position()                          */
+  float view_inv[16];
+  float proj_inv[16];
+  float light_pos[3];        /* Renderer::lightPos  (src/raytracing.hpp:103) */
+  int32_t shading_mode;      /* rt_shading_mode     (src/raytracing.hpp:106) */
+  int32_t enable_shadows;    /* Renderer::enableShadows      (:104)          */
+  int32_t enable_reflections;/* Renderer::enableReflections  (:105)          */
+  int32_t reserved;          /* must be 0 */
+} rt_render_params;
+
+/* Row-band tiling for multi-GPU rendering: image rows are cut into bands of
+ * band_rows rows; band b belongs to rank (b % num_ranks). A rank renders only
+ * its bands and writes them PACKED (its bands in increasing order, each band
+ * W*band_rows pixels, the last band possibly shorter). rank=0,num_ranks=1
+ * renders the full frame in natural layout. */
+typedef struct rt_tile {
+  int32_t band_rows;
+  int32_t rank;
+  int32_t num_ranks;
+  int32_t reserved;
+} rt_tile;
+
+/* ---- errors / device ---------------------------------------------------- */
+const char *rt_last_error(void);
+int rt_abi_version(void);
+/* Number of visible HIP devices (0 if none); never fails. */
+int rt_device_count(void);
+/* Select the HIP device used by subsequent scene creation on this thread. */
+int rt_set_device(int device);
+
+/* ---- host-side inputs (loaders; mirror the reference loaders) ----------- */
+/* cmesh4::LoadMeshFromObj (src/core/mesh.cpp:178-287) [+ loadAndScale,
+ * src/main.cpp:326-343, when scale != 0]. Two-call protocol: call with
+ * vpos4 = idx = NULL to get the counts, then with buffers of that size.
+ * vpos4: float[4*nverts] (x,y,z,w), idx: uint32[nidx]. */
+int rt_load_obj(const char *path, int scale, float *vpos4, int64_t *nverts, uint32_t *idx,
+                int64_t *nidx);
+/* loadSDFGrid (src/grid_raytracing.cpp:127-134): 12-byte header uint32 size[3],
+ * then float values[size.x*size.y*size.z], index (x*sy+y)*sz+z. Two-call protocol. */
+int rt_load_grid(const char *path, uint32_t size[3], float *values);
+/* loadSDFOctree (src/octree_raytracing.cpp:8-16): uint32 count, then count x
+ * 36-byte SDFOctreeNode {float values[8]; uint32 childrenOffset}. Two-call protocol. */
+int rt_load_octree(const char *path, int64_t *count, void *nodes36);
+
+/* Camera(pos, target, up).lookAtMatrix() inverse and perspective inverse,
+ * following src/camera.cpp:36-62 + LiteMath ("unpinned"). */
+int rt_camera(const float pos[3], const float target[3], const float up[3], float fovy_deg,
+              float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]);
+
+/* Host-only: build the BVH8 exactly as rt_scene_create_mesh does and export it
+ * in canonical pre-order (52 x uint32 per node: isLeaf, realCount|count,
+ * startIndex, 0, then the reference Box8 SoA as float bits, +inf in unused
+ * slots, zeros for leaves) plus the triangle permutation (original triangle id
+ * per triangle slot, i.e. BVHBuilder's reordered mesh.indices / 3). Two-call
+ * protocol on *nnodes. Used to check the tree against the reference's. */
+int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                  uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth);
+
+/* ---- scenes ------------------------------------------------------------- */
+/* BVHBuilder::perform (src/triangles_raytracing.cpp:227-258): builds the same
+ * 8-wide SAH BVH on the host, then uploads a GPU layout of it. */
+int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                         rt_scene **out);
+/* SDFGrid (src/grid_raytracing.hpp:10-21). values: x-major, float[sx*sy*sz]. */
+int rt_scene_create_grid(const uint32_t size[3], const float *values, rt_scene **out);
+/* SDFOctree (src/octree_raytracing.hpp:20-47). nodes36: count x 36 bytes. */
+int rt_scene_create_octree(const void *nodes36, int64_t count, rt_scene **out);
+/* SceneUnion(scene, Plane(normal, offset)) (src/raytracing.hpp:83-97,119-186;
+ * src/main.cpp:189-190). enabled=0 renders the scene alone. */
+int rt_scene_set_plane(rt_scene *s, int enabled, const float normal[3], float offset);
+int rt_scene_kind(const rt_scene *s);
+/* Device bytes held by the scene (nodes/triangles/voxels). */
+int64_t rt_scene_device_bytes(const rt_scene *s);
+/* Statistics of the host BVH (mesh scenes): node count, inner count, max depth. */
+int rt_scene_bvh_stats(const rt_scene *s, int64_t *nodes, int64_t *inner, int32_t *max_depth);
+int rt_scene_destroy(rt_scene *s);
+
+/* ---- frames ------------------------------------------------------------- */
+/* Renderer::draw on HOST buffers color[W*H] (RGBA8 packed, R in the low byte)
+ * and t[W*H] (row-major y*W+x). Uploads, renders, downloads, synchronises.
+ * *ms (optional) receives the kernel time in milliseconds (HIP events). */
+int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W,
+              int32_t H, uint32_t flags, float *ms);
+/* Same on DEVICE buffers, asynchronously on `stream` (hipStream_t or NULL).
+ * With tile != NULL only this rank's bands are rendered, packed (rt_tile). */
+int rt_render_device(rt_scene *s, const rt_render_params *p, uint32_t *d_color, float *d_t,
+                     int32_t W, int32_t H, uint32_t flags, const rt_tile *tile, void *stream);
+/* Scatter gathered packed bands of all ranks (ranks x per-rank capacity, as
+ * produced by rt_render_device with a tile) into a natural-layout frame, on
+ * the device. per_rank_pixels = capacity of one rank's packed slot. */
+int rt_untile_device(const uint32_t *d_packed_color, const float *d_packed_t, int64_t per_rank_pixels,
+                     uint32_t *d_color, float *d_t, int32_t W, int32_t H, const rt_tile *tile,
+                     void *stream);
+/* Pixels a rank owns under `tile` (its packed buffer length). */
+int64_t rt_tile_pixels(int32_t W, int32_t H, const rt_tile *tile);
+
+/* ---- rays (IScene::intersect) ------------------------------------------- */
+/* Batch of n rays, host buffers. hit[i] (0/1), t[i], normal[3i..3i+2] exactly
+ * as HitInfo (src/raytracing.hpp:67-73; normal NOT flipped toward the ray),
+ * prim[i] = primitive id (mesh: original triangle index in OBJ face order;
+ * grid: linear index of the c0 cell of the hit sample; octree: leaf node
+ * index; plane: -2; miss: -1). */
+int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, float tnear,
+                      float tfar, int32_t *hit, float *t, float *normal, int64_t *prim);
+
+/* Timing helper for benchmarks: renders `frames` frames back to back on the
+ * device (buffers owned by the library), returns the mean kernel ms per frame
+ * and the total in *total_ms. params[frames] gives one camera per frame. */
+int rt_bench_frames(rt_scene *s, const rt_render_params *params, int32_t frames, int32_t W,
+                    int32_t H, uint32_t flags, float *mean_ms, float *total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTAMD_H */

@@ -1,0 +1,190 @@
+"""ctypes binding of the oracle (oracle/cpuref.cpp) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the parity checker / CPU baseline. The product path
+(triangles-sdf-cpu-raytracing_amd/) never imports it.
+
+Everything here is host memory + numpy. The C functions restate the reference
+hot path; see the header of cpuref.cpp for the file:line map.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libcpuref.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        vp, i64, i32, f32, f64 = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_double
+        P = C.POINTER
+        L.cpuref_load_obj.restype = vp
+        L.cpuref_load_obj.argtypes = [C.c_char_p, C.c_int, P(i64), P(i64)]
+        L.cpuref_mesh_copy.argtypes = [vp, vp, vp]
+        L.cpuref_mesh_free.argtypes = [vp]
+        L.cpuref_scene_mesh.restype = vp
+        L.cpuref_scene_mesh.argtypes = [vp, i64, vp, i64]
+        L.cpuref_scene_grid.restype = vp
+        L.cpuref_scene_grid.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, vp]
+        L.cpuref_scene_octree.restype = vp
+        L.cpuref_scene_octree.argtypes = [vp, i64]
+        L.cpuref_scene_set_plane.argtypes = [vp, C.c_int, vp, f32]
+        L.cpuref_scene_free.argtypes = [vp]
+        L.cpuref_bvh_node_count.restype = i64
+        L.cpuref_bvh_node_count.argtypes = [vp]
+        L.cpuref_bvh_export.restype = i64
+        L.cpuref_bvh_export.argtypes = [vp, vp, i64]
+        L.cpuref_bvh_indices.argtypes = [vp, vp, vp]
+        L.cpuref_camera.argtypes = [vp, vp, vp, f32, f32, f32, f32, vp, vp]
+        L.cpuref_render.restype = f64
+        L.cpuref_render.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+        L.cpuref_intersect_rays.argtypes = [vp, vp, vp, i64, f32, f32, vp, vp, vp, vp]
+        L.cpuref_fnv1a64.restype = C.c_uint64
+        L.cpuref_fnv1a64.argtypes = [vp, i64]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class RefParams(C.Structure):
+    """Same layout as rt_render_params (include/rtamd.h)."""
+    _fields_ = [
+        ("camera_pos", C.c_float * 3),
+        ("view_inv", C.c_float * 16),
+        ("proj_inv", C.c_float * 16),
+        ("light_pos", C.c_float * 3),
+        ("shading_mode", C.c_int32),
+        ("enable_shadows", C.c_int32),
+        ("enable_reflections", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+def load_obj(path: str, scale: bool = True):
+    """cmesh4::LoadMeshFromObj + loadAndScale (main.cpp:326-343) -> (vpos4 [N,4] f32, idx [M] u32)."""
+    L = lib()
+    nv, ni = C.c_int64(), C.c_int64()
+    h = L.cpuref_load_obj(path.encode(), int(scale), C.byref(nv), C.byref(ni))
+    if not h:
+        raise IOError(f"cannot load {path}")
+    v = np.empty((nv.value, 4), np.float32)
+    i = np.empty(ni.value, np.uint32)
+    L.cpuref_mesh_copy(h, _p(v), _p(i))
+    L.cpuref_mesh_free(h)
+    return v, i
+
+
+def camera_matrices(pos, target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0), fovy=45.0, aspect=16 / 9,
+                    znear=0.01, zfar=100.0):
+    """(view_inv, proj_inv) as column-major float32[16] (main.cpp:198-201, raytracing.cpp:73-75)."""
+    vi = np.zeros(16, np.float32)
+    pi = np.zeros(16, np.float32)
+    a = lambda x: np.asarray(x, np.float32)
+    p, t, u = a(pos), a(target), a(up)
+    lib().cpuref_camera(_p(p), _p(t), _p(u), fovy, aspect, znear, zfar, _p(vi), _p(pi))
+    return vi, pi
+
+
+def make_params(cam_pos, view_inv, proj_inv, light=(2.0, 2.0, 2.0), mode=0, shadows=True,
+                reflections=True) -> RefParams:
+    P = RefParams()
+    P.camera_pos[:] = [float(x) for x in cam_pos]
+    P.view_inv[:] = [float(x) for x in view_inv]
+    P.proj_inv[:] = [float(x) for x in proj_inv]
+    P.light_pos[:] = [float(x) for x in light]
+    P.shading_mode = int(mode)
+    P.enable_shadows = int(bool(shadows))
+    P.enable_reflections = int(bool(reflections))
+    return P
+
+
+class RefScene:
+    def __init__(self, handle):
+        self.h = handle
+
+    @staticmethod
+    def mesh(vpos4, idx):
+        vpos4 = np.ascontiguousarray(vpos4, np.float32)
+        idx = np.ascontiguousarray(idx, np.uint32)
+        return RefScene(lib().cpuref_scene_mesh(_p(vpos4), len(vpos4), _p(idx), len(idx)))
+
+    @staticmethod
+    def grid(size, values):
+        values = np.ascontiguousarray(values, np.float32)
+        return RefScene(lib().cpuref_scene_grid(int(size[0]), int(size[1]), int(size[2]), _p(values)))
+
+    @staticmethod
+    def octree(nodes_bytes: np.ndarray):
+        nb = np.ascontiguousarray(nodes_bytes)
+        return RefScene(lib().cpuref_scene_octree(_p(nb), nb.nbytes // 36))
+
+    def set_plane(self, enabled=True, normal=(0.0, 1.0, 0.0), offset=-1.0):
+        n = np.asarray(normal, np.float32)
+        lib().cpuref_scene_set_plane(self.h, int(enabled), _p(n), float(offset))
+
+    def bvh_export(self):
+        L = lib()
+        n = L.cpuref_bvh_node_count(self.h)
+        out = np.zeros((n, 52), np.uint32)
+        m = L.cpuref_bvh_export(self.h, _p(out), n)
+        return out[:m]
+
+    def bvh_indices(self, n_idx):
+        idx = np.zeros(n_idx, np.uint32)
+        tri = np.zeros(n_idx // 3, np.uint32)
+        lib().cpuref_bvh_indices(self.h, _p(idx), _p(tri))
+        return idx, tri
+
+    def render(self, params: RefParams, W: int, H: int, color=None, t=None, prim=False, rows=None,
+               threads: int = 0):
+        """Renderer::draw into (color u32[H,W], t f32[H,W]); returns (color, t, prim|None, ms)."""
+        if color is None:
+            color = np.zeros((H, W), np.uint32)
+        if t is None:
+            t = np.full((H, W), np.inf, np.float32)
+        pr = np.full((H, W), -1, np.int64) if prim else None
+        r0, r1 = (0, H) if rows is None else rows
+        ms = lib().cpuref_render(self.h, C.byref(params), _p(color), _p(t), _p(pr), W, H, r0, r1,
+                                 threads, None)
+        return color, t, pr, ms
+
+    def intersect_rays(self, o, d, tnear=0.01, tfar=100.0):
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        n = len(o)
+        hit = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        prim = np.zeros(n, np.int64)
+        lib().cpuref_intersect_rays(self.h, _p(o), _p(d), n, tnear, tfar, _p(hit), _p(t), _p(nrm),
+                                    _p(prim))
+        return hit, t, nrm, prim
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.cpuref_scene_free(self.h)
+            self.h = None
+
+
+def fnv1a64_words(color: np.ndarray) -> str:
+    """Word-wise FNV-1a-64 over the colour buffer in y*W+x order."""
+    c = np.ascontiguousarray(color, np.uint32).ravel()
+    return f"{lib().cpuref_fnv1a64(_p(c), c.size):016x}"

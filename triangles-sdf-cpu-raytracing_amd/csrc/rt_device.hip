@@ -1,0 +1,769 @@
+// rt_device.hip -- HIP kernels (gfx950) and the C ABI (include/rtamd.h).
+//
+// One thread per pixel; a 256-thread workgroup renders a 16x16 pixel block as
+// four 8x8 wave tiles (coherent rays share BVH / octree nodes and grid
+// voxels in L1/L2). Framebuffer stores are row-major, so a wave writes 8 rows
+// x 32 B per buffer. Per-lane traversal stacks live in LDS, lane-interleaved.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtamd.h"
+#include "rt_host.h"
+#include "rt_layout.h"
+#include "rt_math.h"
+#include "rt_scenes.h"
+
+using namespace rtd;
+
+namespace {
+
+thread_local std::string g_err;
+int set_err(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err(RT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
+constexpr int kTile = 16;
+
+struct FrameArgs {
+  rt_render_params P;
+  uint32_t *color;
+  float *t;
+  int32_t W, H;
+  uint32_t flags;
+  int32_t band_rows, rank, nranks, rows_local;
+};
+
+// ---------------------------------------------------------- scene adapters --
+struct MeshS {
+  MeshDev d;
+  template <int B>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
+    return mesh_intersect<B>(d, o, dir, tn, tf, st);
+  }
+  template <int B>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
+    return mesh_occluded<B>(d, o, dir, tn, tf, st);
+  }
+};
+struct GridS {
+  GridDev d;
+  template <int B>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B>) const {
+    return grid_intersect(d, o, dir, tn, tf);
+  }
+  template <int B>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B>) const {
+    return grid_occluded(d, o, dir, tn, tf);
+  }
+};
+struct OctS {
+  OctDev d;
+  template <int B>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
+    return oct_intersect<B>(d, o, dir, tn, tf, st);
+  }
+  template <int B>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
+    return oct_occluded<B>(d, o, dir, tn, tf, st);
+  }
+};
+
+// SceneUnion(scene, plane)::intersect (raytracing.hpp:87-93): both are
+// intersected, the smaller t wins, ties go to the plane.
+struct SurfHit {
+  Hit h;
+  float albedo;   // grey albedo: mesh/SDF 1.0, plane checker 0.0 / 1.0
+  float refl;     // reflectiveness: plane 0.3, else 0
+};
+template <class S, int B>
+__device__ __forceinline__ SurfHit union_intersect(const S &sc, const PlaneDev &pl, f3 o, f3 d,
+                                                   float tn, float tf, LdsStack<B> st) {
+  SurfHit r{sc.template intersect<B>(o, d, tn, tf, st), 1.0f, 0.0f};
+  if (pl.on) {
+    float tp = kInf, ap = 1.0f;
+    const bool ph = plane_hit(pl, o, d, tn, tf, tp, ap);
+    if (!(r.h.t < (ph ? tp : kInf))) {
+      if (ph) {
+        r.h = Hit{true, tp, pl.n, -2};
+        r.albedo = ap;
+        r.refl = 0.3f;
+      } else {
+        r.h = miss_hit();
+        r.albedo = 1.0f;
+        r.refl = 0.0f;
+      }
+    }
+  }
+  return r;
+}
+// Shadow query: HitInfo::hitten of the union is the OR of both hitten flags.
+template <class S, int B>
+__device__ __forceinline__ bool union_occluded(const S &sc, const PlaneDev &pl, f3 o, f3 d, float tn,
+                                               float tf, LdsStack<B> st) {
+  if (sc.template occluded<B>(o, d, tn, tf, st)) return true;
+  if (pl.on) {
+    float tp, ap;
+    return plane_hit(pl, o, d, tn, tf, tp, ap);
+  }
+  return false;
+}
+
+// Renderer::intersectionColor (raytracing.cpp:13-65) for one ray; the one
+// reflection bounce (maxDepth 2 -> 1) is expanded in place, no recursion.
+template <class S, int B>
+__device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const rt_render_params &P,
+                                        f3 o, f3 d, float tFarEff, bool allow_refl, bool &hit,
+                                        float &t_out, LdsStack<B> st, int64_t *prim);
+
+template <class S, int B>
+__device__ __forceinline__ f4 lambert_color(const S &sc, const PlaneDev &pl,
+                                            const rt_render_params &P, f3 o, f3 d,
+                                            const SurfHit &sh, f3 n, LdsStack<B> st) {
+  bool visible = true;
+  const f3 point = o + sh.h.t * d;
+  const f3 L{P.light_pos[0], P.light_pos[1], P.light_pos[2]};
+  if (P.enable_shadows) {
+    const f3 sd = normalize(L - point);
+    visible = !union_occluded<S, B>(sc, pl, point + 0.3f * sd, sd, 0.01f, 100.0f, st);
+  }
+  const float a = sh.albedo;
+  if (!visible) return f4{a * 0.1f, a * 0.1f, a * 0.1f, 1.0f};
+  const f3 ld = normalize(point - L);
+  const float lam = std_max(dot(-ld, n), 0.0f);  // Lambert (raytracing.cpp:8-11)
+  const f3 c = f3{a * 0.1f, a * 0.1f, a * 0.1f} + lam * f3{a, a, a};
+  return f4{std_min(c.x, 1.0f), std_min(c.y, 1.0f), std_min(c.z, 1.0f), 1.0f};
+}
+
+template <class S, int B>
+__device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const rt_render_params &P,
+                                        f3 o, f3 d, float tFarEff, bool allow_refl, bool &hit,
+                                        float &t_out, LdsStack<B> st, int64_t *prim) {
+  const SurfHit sh = union_intersect<S, B>(sc, pl, o, d, 0.01f, tFarEff, st);
+  if (prim) *prim = sh.h.hit ? sh.h.prim : -1;
+  if (!sh.h.hit) {
+    hit = false;
+    t_out = kInf;
+    return f4{0.0f, 0.0f, 0.0f, 1.0f};
+  }
+  hit = true;
+  t_out = sh.h.t;
+  f3 n = sh.h.n;
+  if (dot(n, d) > 0) n = n * -1.0f;
+  f4 c;
+  if (P.shading_mode == RT_SHADING_NORMAL) {
+    c = f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
+  } else if (P.shading_mode == RT_SHADING_COLOR) {
+    c = f4{sh.albedo, sh.albedo, sh.albedo, 1.0f};
+  } else {
+    c = lambert_color<S, B>(sc, pl, P, o, d, sh, n, st);
+    if (allow_refl && P.enable_reflections && sh.refl > 0.0f) {
+      const float dn = dot(d, n);
+      const f3 R = normalize(n * dn * (-2.0f) + d);  // LiteMath reflect(dir, normal)
+      const f3 point = o + sh.h.t * d;
+      // recursive call with maxDepth 1, tPrev = +inf (raytracing.cpp:51-61)
+      const SurfHit rh = union_intersect<S, B>(sc, pl, point + 0.02f * R, R, 0.01f, 100.0f, st);
+      f4 rc{0.0f, 0.0f, 0.0f, 1.0f};
+      if (rh.h.hit) {
+        f3 rn = rh.h.n;
+        if (dot(rn, R) > 0) rn = rn * -1.0f;
+        rc = lambert_color<S, B>(sc, pl, P, point + 0.02f * R, R, rh, rn, st);
+      }
+      const float r = sh.refl, k = 1.0f - sh.refl;
+      c = f4{c.x * k + r * rc.x, c.y * k + r * rc.y, c.z * k + r * rc.z, c.w * k + r * rc.w};
+    }
+  }
+  return c;
+}
+
+__device__ __forceinline__ int image_row(int yl, const FrameArgs &fa) {
+  if (fa.nranks <= 1) return yl;
+  const int k = yl / fa.band_rows, r = yl - k * fa.band_rows;
+  return (k * fa.nranks + fa.rank) * fa.band_rows + r;
+}
+
+// Renderer::draw (raytracing.cpp:67-102). GENERAL=false is the primary-ray
+// path (Normal shading, no plane, no secondary rays) used by the headline
+// benchmark; GENERAL=true runs intersectionColor in full.
+template <class S, int MAXD, bool GENERAL>
+__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa) {
+  __shared__ uint32_t stk[MAXD * 3 * kBlock];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
+  const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  if (xo >= fa.W || yl >= fa.rows_local) return;
+  LdsStack<kBlock> st{stk + threadIdx.x};
+  const int yo = image_row(yl, fa);
+  const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
+  const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
+  const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+  const size_t idx = (size_t)yl * fa.W + xo;
+  const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
+  const float tPrev = clear ? kInf : fa.t[idx];
+  const float tFarEff = std_min(100.0f, tPrev);  // std::min(tFar, tPrev)
+  bool hit;
+  float t;
+  f4 c;
+  if (!GENERAL) {
+    const Hit h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st);
+    hit = h.hit;
+    t = h.t;
+    f3 n = h.n;
+    if (dot(n, d) > 0) n = n * -1.0f;
+    c = f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
+  } else {
+    c = shade_one<S, kBlock>(sc, pl, fa.P, o, d, tFarEff, true, hit, t, st, nullptr);
+  }
+  // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
+  const bool store = hit && !__builtin_isinf(t);
+  if (clear) {
+    fa.color[idx] = store ? pack_rgba(c) : 0u;
+    fa.t[idx] = store ? t : kInf;
+  } else if (store) {
+    fa.color[idx] = pack_rgba(c);
+    fa.t[idx] = t;
+  }
+}
+
+// IScene::intersect over a batch of rays (union with the plane if enabled).
+template <class S, int MAXD>
+__global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const float *o3,
+                                                       const float *d3, int64_t n, float tn,
+                                                       float tf, int32_t *hit, float *t,
+                                                       float *nrm, int64_t *prim) {
+  __shared__ uint32_t stk[MAXD * 3 * kBlock];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  LdsStack<kBlock> st{stk + threadIdx.x};
+  const f3 o{o3[3 * i], o3[3 * i + 1], o3[3 * i + 2]};
+  const f3 d{d3[3 * i], d3[3 * i + 1], d3[3 * i + 2]};
+  const SurfHit sh = union_intersect<S, kBlock>(sc, pl, o, d, tn, tf, st);
+  hit[i] = sh.h.hit ? 1 : 0;
+  t[i] = sh.h.t;
+  nrm[3 * i] = sh.h.n.x;
+  nrm[3 * i + 1] = sh.h.n.y;
+  nrm[3 * i + 2] = sh.h.n.z;
+  prim[i] = sh.h.hit ? sh.h.prim : -1;
+}
+
+__global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
+                              float *t, int W, int H, int band_rows, int nranks) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)W * H) return;
+  const int yo = (int)(i / W), x = (int)(i - (int64_t)yo * W);
+  const int b = yo / band_rows, r = b % nranks, k = b / nranks;
+  const int64_t src = (int64_t)r * per_rank + ((int64_t)k * band_rows + (yo - b * band_rows)) * W + x;
+  if (c) c[i] = pc[src];
+  if (t) t[i] = pt[src];
+}
+
+}  // namespace
+
+// ================================================================== C ABI ==
+struct rt_scene {
+  int kind = 0;
+  int device = 0;
+  int32_t maxd = 1;  // LDS stack frames the kernel is instantiated for
+  // mesh
+  rtl::GNode *d_nodes = nullptr;
+  rtl::GTri *d_tris = nullptr;
+  uint32_t root = rtl::kInvalidChild;
+  int64_t host_nodes = 0, host_inner = 0;
+  int32_t bvh_depth = 0;
+  // grid
+  float *d_vals = nullptr;
+  uint32_t size[3] = {0, 0, 0};
+  // octree
+  uint32_t *d_child = nullptr;
+  rtl::OctVals *d_ovals = nullptr;
+  int32_t oct_depth = 0;
+  PlaneDev plane{};
+  int64_t dev_bytes = 0;
+  // cached buffers for host-buffer entry points
+  uint32_t *d_color = nullptr;
+  float *d_t = nullptr;
+  size_t fb_cap = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+int pick_maxd(int depth, int32_t &maxd) {
+  // LDS frames per lane: MAXD*12 B; 32 levels = 96 KiB per 256-lane workgroup.
+  const int options[] = {8, 16, 32};
+  for (int m : options)
+    if (depth <= m) { maxd = m; return RT_OK; }
+  return set_err(RT_E_INVALID, "tree deeper than 32 levels");
+}
+
+int ensure_events(rt_scene *s) {
+  if (!s->ev0) HIP_TRY(hipEventCreate(&s->ev0));
+  if (!s->ev1) HIP_TRY(hipEventCreate(&s->ev1));
+  return RT_OK;
+}
+
+int ensure_fb(rt_scene *s, size_t px) {
+  if (px <= s->fb_cap) return RT_OK;
+  if (s->d_color) (void)hipFree(s->d_color);
+  if (s->d_t) (void)hipFree(s->d_t);
+  s->d_color = nullptr;
+  s->d_t = nullptr;
+  s->fb_cap = 0;
+  HIP_TRY(hipMalloc(&s->d_color, px * 4));
+  HIP_TRY(hipMalloc(&s->d_t, px * 4));
+  s->fb_cap = px;
+  return RT_OK;
+}
+
+template <class S, int MAXD>
+void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool general,
+                     hipStream_t stream) {
+  const dim3 grid((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
+  if (general)
+    render_kernel<S, MAXD, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa);
+  else
+    render_kernel<S, MAXD, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa);
+}
+
+int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
+  const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
+  if (s->kind == RT_SCENE_MESH) {
+    MeshS sc{MeshDev{s->d_nodes, s->d_tris, s->root}};
+    switch (s->maxd) {
+      case 8: launch_render_t<MeshS, 8>(sc, s->plane, fa, general, stream); break;
+      case 16: launch_render_t<MeshS, 16>(sc, s->plane, fa, general, stream); break;
+      default: launch_render_t<MeshS, 32>(sc, s->plane, fa, general, stream); break;
+    }
+  } else if (s->kind == RT_SCENE_GRID) {
+    GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
+    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream);
+  } else if (s->kind == RT_SCENE_OCTREE) {
+    OctS sc{OctDev{s->d_child, s->d_ovals}};
+    switch (s->maxd) {
+      case 8: launch_render_t<OctS, 8>(sc, s->plane, fa, general, stream); break;
+      case 16: launch_render_t<OctS, 16>(sc, s->plane, fa, general, stream); break;
+      default: launch_render_t<OctS, 32>(sc, s->plane, fa, general, stream); break;
+    }
+  } else {
+    return set_err(RT_E_STATE, "scene has no geometry");
+  }
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+int check_params(const rt_render_params *p, int32_t W, int32_t H) {
+  if (!p) return set_err(RT_E_INVALID, "params is NULL");
+  if (W <= 0 || H <= 0 || (int64_t)W * H > (int64_t)1 << 31) return set_err(RT_E_INVALID, "bad frame size");
+  if (p->shading_mode < 0 || p->shading_mode > 2) return set_err(RT_E_INVALID, "bad shading mode");
+  return RT_OK;
+}
+
+int fill_frame(FrameArgs &fa, const rt_render_params *p, uint32_t *c, float *t, int32_t W, int32_t H,
+               uint32_t flags, const rt_tile *tile) {
+  fa.P = *p;
+  fa.color = c;
+  fa.t = t;
+  fa.W = W;
+  fa.H = H;
+  fa.flags = flags;
+  fa.band_rows = H;
+  fa.rank = 0;
+  fa.nranks = 1;
+  fa.rows_local = H;
+  if (tile && tile->num_ranks > 1) {
+    if (tile->band_rows <= 0 || tile->rank < 0 || tile->rank >= tile->num_ranks)
+      return set_err(RT_E_INVALID, "bad tile");
+    fa.band_rows = tile->band_rows;
+    fa.rank = tile->rank;
+    fa.nranks = tile->num_ranks;
+    fa.rows_local = (int32_t)(rt_tile_pixels(W, H, tile) / W);
+  }
+  return RT_OK;
+}
+
+template <class S, int MAXD>
+void launch_rays_t(const S &sc, const PlaneDev &pl, const float *o, const float *d, int64_t n,
+                   float tn, float tf, int32_t *hit, float *t, float *nrm, int64_t *prim) {
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  rays_kernel<S, MAXD><<<(unsigned)blocks, kBlock>>>(sc, pl, o, d, n, tn, tf, hit, t, nrm, prim);
+}
+
+}  // namespace
+
+namespace {
+int new_scene(rt_scene **out) {
+  if (!out) return set_err(RT_E_INVALID, "out is NULL");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  rt_scene *s = new rt_scene();
+  s->device = dev;
+  s->plane.on = 0;
+  s->plane.n = f3{0.0f, 1.0f, 0.0f};
+  *out = s;
+  return RT_OK;
+}
+
+template <class T>
+int upload(T **dst, const T *src, size_t n, int64_t &bytes) {
+  if (n == 0) n = 1;  // keep a valid pointer
+  HIP_TRY(hipMalloc(dst, n * sizeof(T)));
+  if (src) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  bytes += (int64_t)(n * sizeof(T));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RTAMD_ABI_VERSION; }
+
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rt_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return RT_OK;
+}
+
+int rt_load_obj(const char *path, int scale, float *vpos4, int64_t *nverts, uint32_t *idx,
+                int64_t *nidx) {
+  if (!path || !nverts || !nidx) return set_err(RT_E_INVALID, "NULL argument");
+  rth::Mesh m;
+  std::string err;
+  if (!rth::load_obj(path, scale != 0, m, err)) return set_err(RT_E_IO, err);
+  const int64_t nv = (int64_t)m.vpos4.size() / 4, ni = (int64_t)m.idx.size();
+  if (vpos4 || idx) {
+    if (*nverts < nv || *nidx < ni) return set_err(RT_E_INVALID, "buffers too small");
+    if (vpos4) std::memcpy(vpos4, m.vpos4.data(), m.vpos4.size() * 4);
+    if (idx) std::memcpy(idx, m.idx.data(), m.idx.size() * 4);
+  }
+  *nverts = nv;
+  *nidx = ni;
+  return RT_OK;
+}
+
+int rt_load_grid(const char *path, uint32_t size[3], float *values) {
+  if (!path || !size) return set_err(RT_E_INVALID, "NULL argument");
+  std::vector<float> v;
+  uint32_t sz[3];
+  std::string err;
+  if (!rth::load_grid(path, sz, v, err)) return set_err(RT_E_IO, err);
+  if (values) {
+    if ((uint64_t)size[0] * size[1] * size[2] < v.size()) return set_err(RT_E_INVALID, "buffer too small");
+    std::memcpy(values, v.data(), v.size() * 4);
+  }
+  size[0] = sz[0]; size[1] = sz[1]; size[2] = sz[2];
+  return RT_OK;
+}
+
+int rt_load_octree(const char *path, int64_t *count, void *nodes36) {
+  if (!path || !count) return set_err(RT_E_INVALID, "NULL argument");
+  std::vector<uint8_t> v;
+  std::string err;
+  if (!rth::load_octree(path, v, err)) return set_err(RT_E_IO, err);
+  const int64_t n = (int64_t)v.size() / 36;
+  if (nodes36) {
+    if (*count < n) return set_err(RT_E_INVALID, "buffer too small");
+    std::memcpy(nodes36, v.data(), v.size());
+  }
+  *count = n;
+  return RT_OK;
+}
+
+int rt_camera(const float pos[3], const float target[3], const float up[3], float fovy_deg,
+              float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]) {
+  if (!pos || !target || !up || !view_inv || !proj_inv) return set_err(RT_E_INVALID, "NULL argument");
+  rth::camera_matrices(pos, target, up, fovy_deg, aspect, znear, zfar, view_inv, proj_inv);
+  return RT_OK;
+}
+
+int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                  uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth) {
+  if (!vpos4 || !idx || !nnodes || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "bad mesh");
+  rth::BVHGpu b;
+  std::string err;
+  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  const int64_t n = (int64_t)b.canon.size() / 52;
+  if (canon) {
+    if (*nnodes < n) return set_err(RT_E_INVALID, "buffer too small");
+    std::memcpy(canon, b.canon.data(), b.canon.size() * 4);
+  }
+  if (perm_tri) std::memcpy(perm_tri, b.perm_tri.data(), b.perm_tri.size() * 4);
+  if (max_depth) *max_depth = b.max_depth;
+  *nnodes = n;
+  return RT_OK;
+}
+
+int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                         rt_scene **out) {
+  if (!vpos4 || !idx || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "empty mesh");
+  rth::BVHGpu b;
+  std::string err;
+  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  int32_t maxd = 8;
+  int rc = pick_maxd(b.max_depth, maxd);
+  if (rc) return rc;
+  rt_scene *s;
+  if ((rc = new_scene(&s))) return rc;
+  s->kind = RT_SCENE_MESH;
+  s->maxd = maxd;
+  s->root = b.root_word;
+  s->host_nodes = b.host_nodes;
+  s->host_inner = b.host_inner;
+  s->bvh_depth = b.max_depth;
+  if ((rc = upload(&s->d_nodes, b.nodes.data(), b.nodes.size(), s->dev_bytes)) ||
+      (rc = upload(&s->d_tris, b.tris.data(), b.tris.size(), s->dev_bytes))) {
+    rt_scene_destroy(s);
+    return rc;
+  }
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_create_grid(const uint32_t size[3], const float *values, rt_scene **out) {
+  if (!size || !values) return set_err(RT_E_INVALID, "NULL argument");
+  const uint64_t n = (uint64_t)size[0] * size[1] * size[2];
+  if (size[0] < 1 || size[1] < 1 || size[2] < 1 || n > (1ull << 32))
+    return set_err(RT_E_INVALID, "bad grid size");
+  rt_scene *s;
+  int rc = new_scene(&s);
+  if (rc) return rc;
+  s->kind = RT_SCENE_GRID;
+  s->size[0] = size[0]; s->size[1] = size[1]; s->size[2] = size[2];
+  if ((rc = upload(&s->d_vals, values, (size_t)n, s->dev_bytes))) {
+    rt_scene_destroy(s);
+    return rc;
+  }
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_create_octree(const void *nodes36, int64_t count, rt_scene **out) {
+  if (!nodes36 || count <= 0) return set_err(RT_E_INVALID, "empty octree");
+  rth::OctGpu g;
+  std::string err;
+  if (!rth::flatten_octree((const uint8_t *)nodes36, count, g, err)) return set_err(RT_E_INVALID, err);
+  int32_t maxd = 8;
+  int rc = pick_maxd(g.max_depth, maxd);
+  if (rc) return rc;
+  rt_scene *s;
+  if ((rc = new_scene(&s))) return rc;
+  s->kind = RT_SCENE_OCTREE;
+  s->maxd = maxd;
+  s->oct_depth = g.max_depth;
+  if ((rc = upload(&s->d_child, g.child.data(), g.child.size(), s->dev_bytes)) ||
+      (rc = upload(&s->d_ovals, g.vals.data(), g.vals.size(), s->dev_bytes))) {
+    rt_scene_destroy(s);
+    return rc;
+  }
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_set_plane(rt_scene *s, int enabled, const float normal[3], float offset) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  PlaneDev &p = s->plane;
+  p.on = enabled ? 1 : 0;
+  if (!enabled) return RT_OK;
+  if (!normal) return set_err(RT_E_INVALID, "normal is NULL");
+  // Plane(normal, offset) + recalcBasis (raytracing.hpp:121-124, 169-179)
+  const float n[3] = {normal[0], normal[1], normal[2]};
+  const float a[3] = {std::fabs(n[0]), std::fabs(n[1]), std::fabs(n[2])};
+  float b1[3];
+  if (a[0] > a[1] && a[0] > a[2]) { b1[0] = n[1]; b1[1] = -n[0]; b1[2] = 0; }
+  else { b1[0] = 0; b1[1] = n[2]; b1[2] = -n[1]; }
+  auto nrm = [](float v[3]) {
+    const float l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    v[0] = v[0] / l; v[1] = v[1] / l; v[2] = v[2] / l;
+  };
+  nrm(b1);
+  float b2[3] = {b1[1] * n[2] - b1[2] * n[1], b1[2] * n[0] - b1[0] * n[2], b1[0] * n[1] - b1[1] * n[0]};
+  nrm(b2);
+  p.n = f3{n[0], n[1], n[2]};
+  p.off = offset;
+  p.b1 = f3{b1[0], b1[1], b1[2]};
+  p.b2 = f3{b2[0], b2[1], b2[2]};
+  return RT_OK;
+}
+
+int rt_scene_kind(const rt_scene *s) { return s ? s->kind : RT_E_INVALID; }
+int64_t rt_scene_device_bytes(const rt_scene *s) { return s ? s->dev_bytes : 0; }
+
+int rt_scene_bvh_stats(const rt_scene *s, int64_t *nodes, int64_t *inner, int32_t *max_depth) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  if (s->kind != RT_SCENE_MESH && s->kind != RT_SCENE_OCTREE) return set_err(RT_E_STATE, "not a tree scene");
+  if (nodes) *nodes = s->host_nodes;
+  if (inner) *inner = s->host_inner;
+  if (max_depth) *max_depth = s->kind == RT_SCENE_MESH ? s->bvh_depth : s->oct_depth;
+  return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene *s) {
+  if (!s) return RT_OK;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(s->device);
+  void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  (void)hipSetDevice(prev);
+  delete s;
+  return RT_OK;
+}
+
+int64_t rt_tile_pixels(int32_t W, int32_t H, const rt_tile *tile) {
+  if (W <= 0 || H <= 0) return 0;
+  if (!tile || tile->num_ranks <= 1) return (int64_t)W * H;
+  if (tile->band_rows <= 0) return 0;
+  int64_t rows = 0;
+  const int32_t nb = (H + tile->band_rows - 1) / tile->band_rows;
+  for (int32_t b = tile->rank; b < nb; b += tile->num_ranks)
+    rows += std::min(tile->band_rows, H - b * tile->band_rows);
+  return rows * W;
+}
+
+int rt_render_device(rt_scene *s, const rt_render_params *p, uint32_t *d_color, float *d_t, int32_t W,
+                     int32_t H, uint32_t flags, const rt_tile *tile, void *stream) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  int rc = check_params(p, W, H);
+  if (rc) return rc;
+  if (!d_color || !d_t) return set_err(RT_E_INVALID, "NULL framebuffer");
+  FrameArgs fa;
+  if ((rc = fill_frame(fa, p, d_color, d_t, W, H, flags, tile))) return rc;
+  if (fa.rows_local <= 0) return RT_OK;
+  return launch_render(s, fa, (hipStream_t)stream);
+}
+
+int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
+              uint32_t flags, float *ms) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  int rc = check_params(p, W, H);
+  if (rc) return rc;
+  if (!color || !t) return set_err(RT_E_INVALID, "NULL framebuffer");
+  const size_t px = (size_t)W * H;
+  if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s))) return rc;
+  if (!(flags & RT_FLAG_CLEAR)) {
+    HIP_TRY(hipMemcpy(s->d_color, color, px * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->d_t, t, px * 4, hipMemcpyHostToDevice));
+  }
+  FrameArgs fa;
+  if ((rc = fill_frame(fa, p, s->d_color, s->d_t, W, H, flags, nullptr))) return rc;
+  HIP_TRY(hipEventRecord(s->ev0, 0));
+  if ((rc = launch_render(s, fa, 0))) return rc;
+  HIP_TRY(hipEventRecord(s->ev1, 0));
+  HIP_TRY(hipMemcpy(color, s->d_color, px * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(t, s->d_t, px * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipEventSynchronize(s->ev1));
+  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  return RT_OK;
+}
+
+int rt_untile_device(const uint32_t *d_packed_color, const float *d_packed_t, int64_t per_rank_pixels,
+                     uint32_t *d_color, float *d_t, int32_t W, int32_t H, const rt_tile *tile,
+                     void *stream) {
+  if (!tile || tile->num_ranks < 1 || tile->band_rows <= 0 || W <= 0 || H <= 0)
+    return set_err(RT_E_INVALID, "bad tile");
+  const int64_t n = (int64_t)W * H;
+  untile_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      d_packed_color, d_packed_t, per_rank_pixels, d_color, d_t, W, H, tile->band_rows, tile->num_ranks);
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, float tnear, float tfar,
+                      int32_t *hit, float *t, float *normal, int64_t *prim) {
+  if (!s || !o || !d || !hit || !t || !normal || !prim) return set_err(RT_E_INVALID, "NULL argument");
+  if (n <= 0) return RT_OK;
+  float *dO = nullptr, *dD = nullptr, *dT = nullptr, *dN = nullptr;
+  int32_t *dH = nullptr;
+  int64_t *dP = nullptr;
+  auto cleanup = [&]() {
+    void *ps[] = {dO, dD, dT, dN, dH, dP};
+    for (void *q : ps)
+      if (q) (void)hipFree(q);
+  };
+  hipError_t e = hipSuccess;
+  do {
+    if ((e = hipMalloc(&dO, n * 12)) || (e = hipMalloc(&dD, n * 12)) || (e = hipMalloc(&dT, n * 4)) ||
+        (e = hipMalloc(&dN, n * 12)) || (e = hipMalloc(&dH, n * 4)) || (e = hipMalloc(&dP, n * 8)))
+      break;
+    if ((e = hipMemcpy(dO, o, n * 12, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(dD, d, n * 12, hipMemcpyHostToDevice)))
+      break;
+    if (s->kind == RT_SCENE_MESH) {
+      MeshS sc{MeshDev{s->d_nodes, s->d_tris, s->root}};
+      switch (s->maxd) {
+        case 8: launch_rays_t<MeshS, 8>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 16: launch_rays_t<MeshS, 16>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        default: launch_rays_t<MeshS, 32>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+      }
+    } else if (s->kind == RT_SCENE_GRID) {
+      GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
+      launch_rays_t<GridS, 1>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP);
+    } else {
+      OctS sc{OctDev{s->d_child, s->d_ovals}};
+      switch (s->maxd) {
+        case 8: launch_rays_t<OctS, 8>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 16: launch_rays_t<OctS, 16>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        default: launch_rays_t<OctS, 32>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+      }
+    }
+    if ((e = hipGetLastError())) break;
+    if ((e = hipMemcpy(hit, dH, n * 4, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(t, dT, n * 4, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(normal, dN, n * 12, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(prim, dP, n * 8, hipMemcpyDeviceToHost)))
+      break;
+  } while (0);
+  cleanup();
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rt_intersect_rays: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+int rt_bench_frames(rt_scene *s, const rt_render_params *params, int32_t frames, int32_t W, int32_t H,
+                    uint32_t flags, float *mean_ms, float *total_ms) {
+  if (!s || !params || frames <= 0) return set_err(RT_E_INVALID, "bad arguments");
+  int rc = check_params(params, W, H);
+  if (rc) return rc;
+  const size_t px = (size_t)W * H;
+  if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s))) return rc;
+  HIP_TRY(hipMemset(s->d_t, 0x7f, px * 4));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipEventRecord(s->ev0, 0));
+  for (int32_t f = 0; f < frames; ++f) {
+    FrameArgs fa;
+    if ((rc = check_params(params + f, W, H)) ||
+        (rc = fill_frame(fa, params + f, s->d_color, s->d_t, W, H, flags, nullptr)) ||
+        (rc = launch_render(s, fa, 0)))
+      return rc;
+  }
+  HIP_TRY(hipEventRecord(s->ev1, 0));
+  HIP_TRY(hipEventSynchronize(s->ev1));
+  float ms = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+  if (total_ms) *total_ms = ms;
+  if (mean_ms) *mean_ms = ms / (float)frames;
+  return RT_OK;
+}
+
+}  // extern "C"

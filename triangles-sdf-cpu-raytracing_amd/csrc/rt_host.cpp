@@ -1,0 +1,641 @@
+// rt_host.cpp -- host-side scene preparation (not on the per-frame path).
+// Build with -ffp-contract=off: the SAH costs and the per-triangle values that
+// are handed to the GPU must round exactly as the reference's.
+#include "rt_host.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <unordered_map>
+#include <utility>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace rth {
+
+static const float kInf = std::numeric_limits<float>::infinity();
+
+// ------------------------------------------------------------- loaders ---
+static bool read_file(const char *path, std::vector<char> &buf, std::string &err) {
+  FILE *f = std::fopen(path, "rb");
+  if (!f) { err = std::string("cannot open ") + path; return false; }
+  std::fseek(f, 0, SEEK_END);
+  long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  if (n < 0) { std::fclose(f); err = "cannot size file"; return false; }
+  buf.resize((size_t)n + 1);
+  size_t got = n ? std::fread(buf.data(), 1, (size_t)n, f) : 0;
+  std::fclose(f);
+  if (got != (size_t)n) { err = "short read"; return false; }
+  buf[(size_t)n] = '\0';
+  return true;
+}
+
+// OBJ -> SimpleMesh with the semantics of cmesh4::LoadMeshFromObj
+// (core/mesh.cpp:178-287 over tinyobjloader v2): 'v x y z' parsed as
+// (float)strtod, face corners 'v', 'v/t', 'v//n', 'v/t/n' with 1-based or
+// negative indices, polygons fanned, vertices de-duplicated on the (v, vn, vt)
+// index tuple in first-use order, w = 1. Optional loadAndScale
+// (main.cpp:326-343): centre the bbox at 0 and divide by |boxMax - center|.
+bool load_obj(const char *path, bool scale, Mesh &out, std::string &err) {
+  std::vector<char> buf;
+  if (!read_file(path, buf, err)) return false;
+  std::vector<float> pos;
+  int64_t n_vn = 0, n_vt = 0;
+  struct Corner { int32_t v, t, n; };
+  std::vector<Corner> corners;
+  std::vector<Corner> poly;
+  auto fix = [](long i, int64_t n) -> int32_t {
+    if (i > 0) return (int32_t)(i - 1);
+    if (i < 0) return (int32_t)(n + i);
+    return -1;
+  };
+  char *p = buf.data();
+  char *end = p + buf.size() - 1;
+  while (p < end) {
+    char *line = p;
+    while (p < end && *p != '\n') ++p;
+    char *eol = p;
+    if (p < end) ++p;
+    *eol = '\0';
+    char *q = line;
+    while (*q == ' ' || *q == '\t') ++q;
+    if (q[0] == 'v' && (q[1] == ' ' || q[1] == '\t')) {
+      char *e = q + 2;
+      for (int k = 0; k < 3; ++k) { char *s = e; pos.push_back((float)std::strtod(s, &e)); }
+    } else if (q[0] == 'v' && q[1] == 'n' && (q[2] == ' ' || q[2] == '\t')) {
+      ++n_vn;
+    } else if (q[0] == 'v' && q[1] == 't' && (q[2] == ' ' || q[2] == '\t')) {
+      ++n_vt;
+    } else if (q[0] == 'f' && (q[1] == ' ' || q[1] == '\t')) {
+      q += 2;
+      poly.clear();
+      for (;;) {
+        while (*q == ' ' || *q == '\t' || *q == '\r') ++q;
+        if (!*q) break;
+        Corner c{-1, -1, -1};
+        char *e;
+        c.v = fix(std::strtol(q, &e, 10), (int64_t)pos.size() / 3);
+        q = e;
+        if (*q == '/') {
+          ++q;
+          if (*q != '/') { c.t = fix(std::strtol(q, &e, 10), n_vt); q = e; }
+          if (*q == '/') { ++q; c.n = fix(std::strtol(q, &e, 10), n_vn); q = e; }
+        }
+        while (*q && *q != ' ' && *q != '\t' && *q != '\r') ++q;
+        if (c.v < 0 || (int64_t)c.v >= (int64_t)pos.size() / 3) { err = "face index out of range"; return false; }
+        poly.push_back(c);
+      }
+      for (size_t i = 2; i < poly.size(); ++i) {
+        corners.push_back(poly[0]);
+        corners.push_back(poly[i - 1]);
+        corners.push_back(poly[i]);
+      }
+    }
+  }
+  struct KH {
+    size_t operator()(uint64_t k) const { return (size_t)(k * 0x9E3779B97F4A7C15ull); }
+  };
+  // key = (v, t, n) packed; indices are < 2^21 for any mesh this loader accepts
+  std::unordered_map<uint64_t, uint32_t, KH> uniq;
+  uniq.reserve(corners.size());
+  out.vpos4.clear();
+  out.idx.clear();
+  out.idx.reserve(corners.size());
+  for (const Corner &c : corners) {
+    uint64_t key = ((uint64_t)(uint32_t)(c.v + 1)) | ((uint64_t)(uint32_t)(c.t + 1) << 21) |
+                   ((uint64_t)(uint32_t)(c.n + 1) << 42);
+    if (c.v + 1 >= (1 << 21) || c.t + 1 >= (1 << 21) || c.n + 1 >= (1 << 21)) {
+      err = "OBJ too large for this loader";
+      return false;
+    }
+    auto it = uniq.find(key);
+    uint32_t id;
+    if (it != uniq.end()) {
+      id = it->second;
+    } else {
+      id = (uint32_t)(out.vpos4.size() / 4);
+      uniq.emplace(key, id);
+      out.vpos4.push_back(pos[3 * (size_t)c.v]);
+      out.vpos4.push_back(pos[3 * (size_t)c.v + 1]);
+      out.vpos4.push_back(pos[3 * (size_t)c.v + 2]);
+      out.vpos4.push_back(1.0f);
+    }
+    out.idx.push_back(id);
+  }
+  if (out.idx.empty()) { err = "OBJ has no faces"; return false; }
+  if (scale) {
+    // calc_bbox (raytracing.hpp:29-37) then loadAndScale (main.cpp:326-343)
+    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    size_t nv = out.vpos4.size() / 4;
+    for (size_t i = 0; i < nv; ++i) {
+      float w = out.vpos4[4 * i + 3];
+      for (int k = 0; k < 3; ++k) {
+        float c = out.vpos4[4 * i + k] / w;
+        mn[k] = std::min(mn[k], c);
+        mx[k] = std::max(mx[k], c);
+      }
+    }
+    float center[3], d[3];
+    for (int k = 0; k < 3; ++k) center[k] = (mn[k] + mx[k]) / 2.0f;
+    for (int k = 0; k < 3; ++k) d[k] = mx[k] - center[k];
+    float s = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    for (size_t i = 0; i < nv; ++i) {
+      float *v = &out.vpos4[4 * i];
+      float w = v[3];
+      float x = v[0] / w, y = v[1] / w, z = v[2] / w;  // v /= w (w/w == 1 exactly)
+      x = (x - center[0]) / s;
+      y = (y - center[1]) / s;
+      z = (z - center[2]) / s;
+      v[0] = x * w; v[1] = y * w; v[2] = z * w; v[3] = 1.0f * w;
+    }
+  }
+  return true;
+}
+
+// loadSDFGrid (grid_raytracing.cpp:127-134), with the size check the
+// reference omits (12 + 4*sx*sy*sz bytes).
+bool load_grid(const char *path, uint32_t size[3], std::vector<float> &values, std::string &err) {
+  FILE *f = std::fopen(path, "rb");
+  if (!f) { err = std::string("cannot open ") + path; return false; }
+  if (std::fread(size, 4, 3, f) != 3) { std::fclose(f); err = "truncated grid header"; return false; }
+  uint64_t n = (uint64_t)size[0] * size[1] * size[2];
+  if (n == 0 || n > (1ull << 32)) { std::fclose(f); err = "bad grid size"; return false; }
+  values.resize(n);
+  size_t got = std::fread(values.data(), 4, n, f);
+  std::fclose(f);
+  if (got != n) { err = "truncated grid values"; return false; }
+  return true;
+}
+
+// loadSDFOctree (octree_raytracing.cpp:8-16): u32 count + count x 36 B.
+bool load_octree(const char *path, std::vector<uint8_t> &nodes36, std::string &err) {
+  FILE *f = std::fopen(path, "rb");
+  if (!f) { err = std::string("cannot open ") + path; return false; }
+  uint32_t n = 0;
+  if (std::fread(&n, 4, 1, f) != 1) { std::fclose(f); err = "truncated octree header"; return false; }
+  nodes36.resize((size_t)n * 36);
+  size_t got = n ? std::fread(nodes36.data(), 36, n, f) : 0;
+  std::fclose(f);
+  if (got != n) { err = "truncated octree nodes"; return false; }
+  return true;
+}
+
+// ---------------------------------------------------------- BVH8 build ---
+// Same tree as BVHBuilder::perform (triangles_raytracing.cpp:12-258):
+// full-sweep binary SAH on x, y, z (triangles ordered by their bbox max along
+// the axis with std::sort, the reference's par_unseq sort without TBB),
+// EMPTY_NODE_TRAVERSE_COST = 0.2, dividers aligned to 8-triangle multiples,
+// up to 7 binary splits per node taken breadth-first, median fallback.
+// Differences in form only: triangles are sorted as 32-bit ids with
+// precomputed keys (the comparator sees the same values, so std::sort makes
+// the same comparisons and the same permutation), bbox prefix/suffix unions
+// use precomputed per-triangle boxes (min/max are exact), and node storage is
+// renumbered afterwards (the reference's OpenMP task order only moves offsets).
+namespace {
+
+struct Box {
+  float mn[3], mx[3];
+};
+static inline Box empty_box() { return {{kInf, kInf, kInf}, {-kInf, -kInf, -kInf}}; }
+static inline void grow(Box &b, const Box &t) {
+  for (int k = 0; k < 3; ++k) {
+    b.mn[k] = std::min(b.mn[k], t.mn[k]);
+    b.mx[k] = std::max(b.mx[k], t.mx[k]);
+  }
+}
+static inline float surface_area(const Box &b) {  // raytracing.hpp:62-65
+  float dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+  return 2 * (dx * dy + dx * dz + dy * dz);
+}
+
+struct HNode {
+  bool leaf = false;
+  uint32_t start = 0, count = 0;  // leaf: range in indices (reference units)
+  uint32_t nchild = 0;
+  int32_t child[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  Box box[8];
+};
+
+struct Builder {
+  std::vector<uint32_t> cur, scrY, scrZ;  // triangle ids, 'cur' = mesh.indices order
+  std::vector<Box> triBox, leftB, rightB;
+  std::vector<float> key[3];
+  std::vector<HNode> nodes;
+
+  struct Div { bool divided = false; size_t divider = (size_t)-1; float sah = kInf; };
+
+  // triangles_raytracing.cpp:30-117 in index units [start, end)
+  Div try_axis(std::vector<uint32_t> &ids, size_t start, size_t end, int axis) {
+    const float *K = key[axis].data();
+    std::sort(ids.begin() + start / 3, ids.begin() + end / 3,
+              [K](uint32_t a, uint32_t b) { return K[a] < K[b]; });
+    for (size_t b = start / 3; b != end / 3; ++b) {
+      Box &box = leftB[b];
+      box = (b == start / 3) ? empty_box() : leftB[b - 1];
+      grow(box, triBox[ids[b]]);
+    }
+    for (size_t r = start / 3; r != end / 3; ++r) {
+      size_t b = end / 3 - r + start / 3 - 1;
+      Box &box = rightB[b];
+      box = (r == start / 3) ? empty_box() : rightB[b + 1];
+      grow(box, triBox[ids[b]]);
+    }
+    Div res;
+    res.sah = static_cast<float>(end - start) / 3.0f;
+    const float parentSA = surface_area(leftB[end / 3 - 1]);
+    for (size_t d = start + 3; d < end; d += 3) {
+      const float lc = static_cast<float>(d - start) / 3.0f;
+      const float rc = static_cast<float>(end - start) / 3.0f - lc;
+      const float c = 0.2f + surface_area(leftB[d / 3 - 1]) / parentSA * lc +
+                      surface_area(rightB[d / 3]) / parentSA * rc;
+      if (c < res.sah) { res.sah = c; res.divider = d; res.divided = true; }
+    }
+    if (res.divided && (res.divider - start) % 24 != 0) {
+      size_t d1 = (res.divider - 1) / 24 * 24, d2 = ((res.divider - 1) / 24 + 1) * 24;
+      size_t nearest = (res.divider - d1 <= d2 - res.divider) ? d1 : d2;
+      size_t other = d1 + d2 - nearest;
+      if (start < nearest && nearest < end) res.divider = nearest;
+      else if (start < other && other < end) res.divider = other;
+    }
+    return res;
+  }
+
+  // triangles_raytracing.cpp:119-153
+  Div try_divide(size_t start, size_t end) {
+    if (end - start <= 8 * 3) return Div{};
+    std::copy(cur.begin() + start / 3, cur.begin() + end / 3, scrY.begin() + start / 3);
+    std::copy(cur.begin() + start / 3, cur.begin() + end / 3, scrZ.begin() + start / 3);
+    const float curSAH = static_cast<float>(end - start) / 3.0f;
+    Div dx = try_axis(cur, start, end, 0);
+    Div dy = try_axis(scrY, start, end, 1);
+    Div dz = try_axis(scrZ, start, end, 2);
+    const float m = std::min({curSAH, dx.sah, dy.sah, dz.sah});
+    if (dx.sah == m) return dx;
+    if (dy.sah == m) {
+      std::copy(scrY.begin() + start / 3, scrY.begin() + end / 3, cur.begin() + start / 3);
+      return dy;
+    }
+    if (dz.sah == m) {
+      std::copy(scrZ.begin() + start / 3, scrZ.begin() + end / 3, cur.begin() + start / 3);
+      return dz;
+    }
+    return Div{};
+  }
+
+  int32_t alloc_node() {
+    int32_t id;
+#pragma omp critical(rt_bvh_nodes)
+    {
+      id = (int32_t)nodes.size();
+      nodes.emplace_back();
+    }
+    return id;
+  }
+
+  // triangles_raytracing.cpp:155-225
+  void create(int32_t self, size_t start, size_t end) {
+    size_t dividers[20] = {};
+    size_t nd = 0;
+    std::pair<size_t, size_t> q[40];  // ChipQueue<., 40> (triangles_raytracing.hpp:69-97)
+    int qf = 0, qr = -1, qc = 0;
+    auto enq = [&](size_t a, size_t b) {
+      if (qc == 40) return;
+      qr = (qr + 1) % 40;
+      q[qr] = {a, b};
+      ++qc;
+    };
+    enq(start, end);
+    while (qc) {
+      auto c = q[qf];
+      qf = (qf + 1) % 40;
+      --qc;
+      if (nd == 7) break;
+      Div r = try_divide(c.first, c.second);
+      if (r.divided) {
+        dividers[nd++] = r.divider;
+        enq(c.first, r.divider);
+        enq(r.divider, c.second);
+      }
+    }
+    HNode node;
+    if (nd == 0) {
+      if (end - start > 24) {
+        dividers[nd++] = ((start / 3 + end / 3) / 2) * 3;
+      } else {
+        node.leaf = true;
+        node.start = (uint32_t)start;
+        node.count = (uint32_t)(end - start);
+#pragma omp critical(rt_bvh_nodes)
+        nodes[self] = node;
+        return;
+      }
+    }
+    std::sort(dividers, dividers + nd);
+    node.nchild = (uint32_t)(nd + 1);
+    size_t lo[8], hi[8];
+    for (size_t c = 0; c <= nd; ++c) {
+      lo[c] = (c == 0) ? start : dividers[c - 1];
+      hi[c] = (c == nd) ? end : dividers[c];
+      Box b = empty_box();
+      for (size_t t = lo[c] / 3; t < hi[c] / 3; ++t) grow(b, triBox[cur[t]]);
+      node.box[c] = b;
+      node.child[c] = alloc_node();
+    }
+#pragma omp critical(rt_bvh_nodes)
+    nodes[self] = node;
+    for (size_t c = 0; c <= nd; ++c) {
+      const int32_t ch = node.child[c];
+      const size_t a = lo[c], b = hi[c];
+      if (b - a > 3 * 2048) {
+#pragma omp task firstprivate(ch, a, b)
+        create(ch, a, b);
+      } else {
+        create(ch, a, b);
+      }
+    }
+#pragma omp taskwait
+  }
+};
+
+}  // namespace
+
+bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                std::string &err) {
+  if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
+  const size_t ntri = (size_t)nidx / 3;
+  for (int64_t i = 0; i < nidx; ++i)
+    if ((int64_t)idx[i] >= nverts) { err = "vertex index out of range"; return false; }
+  if (ntri > rtl::kMaxLeafFirstTri) { err = "too many triangles"; return false; }
+  out = BVHGpu();
+  if (ntri == 0) { out.root_word = rtl::kInvalidChild; return true; }
+
+  Builder B;
+  B.triBox.resize(ntri);
+  for (int a = 0; a < 3; ++a) B.key[a].resize(ntri);
+  // per-triangle box of the /w-divided vertices (calc_bbox, raytracing.hpp:51-60)
+  for (size_t t = 0; t < ntri; ++t) {
+    Box b = empty_box();
+    for (int k = 0; k < 3; ++k) {
+      const float *v = vpos4 + 4 * (size_t)idx[3 * t + k];
+      const float w = v[3];
+      Box p{{v[0] / w, v[1] / w, v[2] / w}, {v[0] / w, v[1] / w, v[2] / w}};
+      grow(b, p);
+    }
+    B.triBox[t] = b;
+    for (int a = 0; a < 3; ++a) B.key[a][t] = b.mx[a];
+  }
+  B.cur.resize(ntri);
+  for (size_t t = 0; t < ntri; ++t) B.cur[t] = (uint32_t)t;
+  B.scrY.resize(ntri);
+  B.scrZ.resize(ntri);
+  B.leftB.resize(ntri);
+  B.rightB.resize(ntri);
+  B.nodes.reserve(ntri + 16);
+  B.nodes.emplace_back();
+#pragma omp parallel
+  {
+#pragma omp single
+    B.create(0, 0, (size_t)nidx);
+  }
+
+  // ---- canonical export + GPU layout (BFS over inner nodes) -------------
+  const std::vector<HNode> &H = B.nodes;
+  out.host_nodes = (int64_t)H.size();
+  out.perm_tri = B.cur;
+  out.perm_idx.resize((size_t)nidx);
+  for (size_t t = 0; t < ntri; ++t)
+    for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)B.cur[t] + k];
+
+  {  // canonical pre-order (52 u32 per node), same as the oracle's export
+    std::vector<int32_t> st{0};
+    while (!st.empty()) {
+      int32_t id = st.back();
+      st.pop_back();
+      const HNode &n = H[id];
+      uint32_t rec[52] = {};
+      rec[0] = n.leaf;
+      rec[1] = n.leaf ? n.count : n.nchild;
+      rec[2] = n.leaf ? n.start : 0;
+      if (!n.leaf) {
+        float bx[48];
+        for (int c = 0; c < 8; ++c) {
+          const bool v = (uint32_t)c < n.nchild;
+          bx[0 * 8 + c] = v ? n.box[c].mn[0] : kInf;
+          bx[1 * 8 + c] = v ? n.box[c].mn[1] : kInf;
+          bx[2 * 8 + c] = v ? n.box[c].mn[2] : kInf;
+          bx[3 * 8 + c] = v ? n.box[c].mx[0] : kInf;
+          bx[4 * 8 + c] = v ? n.box[c].mx[1] : kInf;
+          bx[5 * 8 + c] = v ? n.box[c].mx[2] : kInf;
+        }
+        std::memcpy(rec + 4, bx, 192);
+        for (int c = (int)n.nchild - 1; c >= 0; --c) st.push_back(n.child[c]);
+      }
+      out.canon.insert(out.canon.end(), rec, rec + 52);
+    }
+  }
+
+  auto leaf_word = [&](const HNode &n) -> uint32_t {
+    const uint32_t first = (uint32_t)out.tris.size();
+    const uint32_t nt = n.count / 3;
+    for (uint32_t k = 0; k < nt; ++k) {
+      const uint32_t slot = n.start / 3 + k;
+      const uint32_t *tv = idx + 3 * (size_t)B.cur[slot];
+      float v[3][3];
+      for (int j = 0; j < 3; ++j) {
+        const float *p = vpos4 + 4 * (size_t)tv[j];
+        const float w = p[3];
+        v[j][0] = p[0] / w; v[j][1] = p[1] / w; v[j][2] = p[2] / w;  // v /= v.w (:307-309)
+      }
+      rtl::GTri g;
+      g.v0x = v[0][0]; g.v0y = v[0][1]; g.v0z = v[0][2];
+      g.orig_id = B.cur[slot];
+      g.e1x = v[1][0] - v[0][0]; g.e1y = v[1][1] - v[0][1]; g.e1z = v[1][2] - v[0][2];
+      g.e2x = v[2][0] - v[0][0]; g.e2y = v[2][1] - v[0][1]; g.e2z = v[2][2] - v[0][2];
+      g.pad1 = g.pad2 = 0.0f;
+      out.tris.push_back(g);
+    }
+    if (nt == 0) return rtl::kInvalidChild;
+    return rtl::kLeafBit | (first << 3) | (nt - 1);
+  };
+
+  if (H[0].leaf) {
+    out.root_word = leaf_word(H[0]);
+    out.max_depth = 0;
+    out.host_inner = 0;
+    return true;
+  }
+  // BFS over inner nodes; depth = number of inner ancestors incl. itself
+  std::vector<int32_t> order{0};
+  std::vector<int32_t> depth_of{1};
+  std::vector<int32_t> gpu_id(H.size(), -1);
+  gpu_id[0] = 0;
+  for (size_t i = 0; i < order.size(); ++i) {
+    const HNode &n = H[order[i]];
+    for (uint32_t c = 0; c < n.nchild; ++c) {
+      const int32_t ch = n.child[c];
+      if (!H[ch].leaf) {
+        gpu_id[ch] = (int32_t)order.size();
+        order.push_back(ch);
+        depth_of.push_back(depth_of[i] + 1);
+      }
+    }
+  }
+  out.host_inner = (int64_t)order.size();
+  out.nodes.resize(order.size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    const HNode &n = H[order[i]];
+    rtl::GNode &g = out.nodes[i];
+    out.max_depth = std::max(out.max_depth, depth_of[i]);
+    for (int c = 0; c < 8; ++c) {
+      if ((uint32_t)c < n.nchild) {
+        for (int k = 0; k < 3; ++k) { g.box[c][k] = n.box[c].mn[k]; g.box[c][3 + k] = n.box[c].mx[k]; }
+        const HNode &ch = H[n.child[c]];
+        g.child[c] = ch.leaf ? leaf_word(ch) : (uint32_t)gpu_id[n.child[c]];
+      } else {
+        for (int k = 0; k < 6; ++k) g.box[c][k] = kInf;
+        g.child[c] = rtl::kInvalidChild;
+      }
+    }
+  }
+  out.root_word = 0;
+  return true;
+}
+
+// --------------------------------------------------------------- octree ---
+bool flatten_octree(const uint8_t *nodes36, int64_t count, OctGpu &out, std::string &err) {
+  out = OctGpu();
+  if (count <= 0) { err = "empty octree"; return false; }
+  out.child.resize((size_t)count);
+  out.vals.resize((size_t)count);
+  for (int64_t i = 0; i < count; ++i) {
+    float v[8];
+    uint32_t off;
+    std::memcpy(v, nodes36 + 36 * i, 32);
+    std::memcpy(&off, nodes36 + 36 * i + 32, 4);
+    std::memcpy(out.vals[(size_t)i].v, v, 32);
+    if (off == 0) {
+      // octree_raytracing.hpp:12-17 isEmpty(), octree_raytracing.cpp:125-133
+      bool all10 = true, all0 = true, allAbove = true;
+      for (int k = 0; k < 8; ++k) {
+        all10 = all10 && (v[k] > 10.0f);
+        all0 = all0 && (v[k] == 0.0f);
+        allAbove = allAbove && (v[k] >= 1e-4f);
+      }
+      out.child[(size_t)i] = (all10 || all0 || allAbove) ? rtl::kOctNeverHits : 0u;
+    } else {
+      if ((int64_t)off + 7 >= count || off == rtl::kOctNeverHits) { err = "octree child offset out of range"; return false; }
+      out.child[(size_t)i] = off;
+    }
+  }
+  // depth (levels of inner nodes on the deepest path), with a cycle guard
+  std::vector<std::pair<uint32_t, int32_t>> st{{0u, 0}};
+  int64_t visited = 0;
+  while (!st.empty()) {
+    auto [n, d] = st.back();
+    st.pop_back();
+    if (++visited > count || d > 24) { err = "octree is cyclic or deeper than 24 levels"; return false; }
+    const uint32_t c = out.child[n];
+    if (c != 0 && c != rtl::kOctNeverHits) {
+      out.max_depth = std::max(out.max_depth, d + 1);
+      for (int k = 0; k < 8; ++k) st.push_back({c + (uint32_t)k, d + 1});
+    }
+  }
+  return true;
+}
+
+// --------------------------------------------------------------- camera ---
+// Reference camera math: Camera(pos, target, up) (camera.cpp:36-62, the
+// quaternion left un-normalised, camera.cpp:61), up() (camera.hpp:29-31),
+// lookAtMatrix() (camera.hpp:24-26) and the LiteMath restatement recorded in
+// SURVEY.md 8(c) for lookAt / perspectiveMatrix / inverse4x4.
+namespace {
+struct V3 { float x, y, z; };
+static inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline float dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline V3 crs(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+static inline V3 nrm(V3 a) { float l = std::sqrt(dot3(a, a)); return {a.x / l, a.y / l, a.z / l}; }
+struct M4 { float m[4][4]; float &at(int r, int c) { return m[c][r]; } };
+static M4 look_at(V3 eye, V3 center, V3 up) {
+  V3 z = nrm(sub(eye, center));
+  V3 x = nrm(crs(up, z));
+  V3 y = nrm(crs(z, x));
+  M4 M{};
+  M.at(0, 0) = x.x; M.at(0, 1) = x.y; M.at(0, 2) = x.z; M.at(0, 3) = -dot3(x, eye);
+  M.at(1, 0) = y.x; M.at(1, 1) = y.y; M.at(1, 2) = y.z; M.at(1, 3) = -dot3(y, eye);
+  M.at(2, 0) = z.x; M.at(2, 1) = z.y; M.at(2, 2) = z.z; M.at(2, 3) = -dot3(z, eye);
+  M.at(3, 3) = 1.0f;
+  return M;
+}
+static void invert(M4 &A, float out[16]) {
+  double a[4][8];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) { a[r][c] = A.at(r, c); a[r][c + 4] = (r == c) ? 1.0 : 0.0; }
+  for (int c = 0; c < 4; ++c) {
+    int p = c;
+    for (int r = c + 1; r < 4; ++r) if (std::fabs(a[r][c]) > std::fabs(a[p][c])) p = r;
+    if (p != c) for (int k = 0; k < 8; ++k) std::swap(a[p][k], a[c][k]);
+    const double piv = a[c][c];
+    for (int k = 0; k < 8; ++k) a[c][k] /= piv;
+    for (int r = 0; r < 4; ++r) {
+      if (r == c) continue;
+      const double f = a[r][c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+    }
+  }
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) out[c * 4 + r] = (float)a[r][c + 4];
+}
+struct Q { float x, y, z, w; };
+static inline Q qmul(Q a, Q b) {  // quaternion.hpp:40-45
+  return {a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+          a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+}  // namespace
+
+void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
+                     float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]) {
+  V3 P{pos[0], pos[1], pos[2]}, T{target[0], target[1], target[2]}, U{up[0], up[1], up[2]};
+  M4 m = look_at(P, T, U);
+  Q q;
+  if (m.at(2, 2) < 0) {
+    if (m.at(0, 0) > m.at(1, 1)) {
+      float t = 1 + m.at(0, 0) - m.at(1, 1) - m.at(2, 2);
+      q = {t, m.at(0, 1) + m.at(1, 0), m.at(2, 0) + m.at(0, 2), m.at(1, 2) - m.at(2, 1)};
+    } else {
+      float t = 1 - m.at(0, 0) + m.at(1, 1) - m.at(2, 2);
+      q = {m.at(0, 1) + m.at(1, 0), t, m.at(1, 2) + m.at(2, 1), m.at(2, 0) - m.at(0, 2)};
+    }
+  } else {
+    if (m.at(0, 0) < -m.at(1, 1)) {
+      float t = 1 - m.at(0, 0) - m.at(1, 1) + m.at(2, 2);
+      q = {m.at(2, 0) + m.at(0, 2), m.at(1, 2) + m.at(2, 1), t, m.at(0, 1) - m.at(1, 0)};
+    } else {
+      float t = 1 + m.at(0, 0) + m.at(1, 1) + m.at(2, 2);
+      q = {m.at(1, 2) - m.at(2, 1), m.at(2, 0) - m.at(0, 2), m.at(0, 1) - m.at(1, 0), t};
+    }
+  }
+  // up() = normalize(rotateVector({0,1,0}, q)) (quaternion.hpp:47-52)
+  Q p{0.0f, 1.0f, 0.0f, 0.0f}, c{-q.x, -q.y, -q.z, q.w};
+  Q r = qmul(qmul(q, p), c);
+  V3 up2 = nrm(V3{r.x, r.y, r.z});
+  M4 view = look_at(P, T, up2);
+  invert(view, view_inv);
+  // perspectiveMatrix(fovy, aspect, near, far)
+  M4 pr{};
+  const float ymax = znear * std::tan(fovy * 3.14159265358979323846f / 360.0f);
+  const float xmax = ymax * aspect;
+  pr.m[0][0] = 2.0f * znear / (2.0f * xmax);
+  pr.m[1][1] = 2.0f * znear / (2.0f * ymax);
+  pr.m[2][2] = (-zfar - znear) / (zfar - znear);
+  pr.m[2][3] = -1.0f;
+  pr.m[3][2] = -2.0f * zfar * znear / (zfar - znear);
+  invert(pr, proj_inv);
+}
+
+}  // namespace rth

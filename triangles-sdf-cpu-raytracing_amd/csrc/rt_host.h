@@ -1,0 +1,48 @@
+// rt_host.h -- host-side scene preparation for the MI355X renderer.
+// Loaders, the BVH8 SAH builder (same tree as BVHBuilder::perform,
+// triangles_raytracing.cpp:227-258) and its GPU layout, octree flattening,
+// and the reference camera math. Compiled by g++ with -ffp-contract=off.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "rt_layout.h"
+
+namespace rth {
+
+struct Mesh {
+  std::vector<float> vpos4;     // 4 floats per vertex (x, y, z, w)
+  std::vector<uint32_t> idx;    // 3 per triangle
+};
+
+bool load_obj(const char *path, bool scale, Mesh &out, std::string &err);
+bool load_grid(const char *path, uint32_t size[3], std::vector<float> &values, std::string &err);
+bool load_octree(const char *path, std::vector<uint8_t> &nodes36, std::string &err);
+
+struct BVHGpu {
+  std::vector<rtl::GNode> nodes;   // inner nodes, BFS order, root = 0
+  std::vector<rtl::GTri> tris;     // leaf triangles, leaves in BFS order of their parents
+  uint32_t root_word = rtl::kInvalidChild;
+  int32_t max_depth = 0;           // inner nodes on the deepest root->leaf path
+  int64_t host_nodes = 0, host_inner = 0;
+  // canonical pre-order export (52 x u32 per node), for parity with the oracle
+  std::vector<uint32_t> canon;
+  std::vector<uint32_t> perm_idx;  // mesh indices after the build's permutation
+  std::vector<uint32_t> perm_tri;  // original triangle id per triangle slot
+};
+bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                std::string &err);
+
+struct OctGpu {
+  std::vector<uint32_t> child;        // per node: 0 leaf, kOctNeverHits, or childrenOffset
+  std::vector<rtl::OctVals> vals;     // per node corner values
+  int32_t max_depth = 0;
+};
+bool flatten_octree(const uint8_t *nodes36, int64_t count, OctGpu &out, std::string &err);
+
+void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
+                     float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]);
+
+}  // namespace rth

@@ -1,0 +1,19 @@
+"""rtamd -- MI355X-native primary-ray renderer (Python binding over include/rtamd.h).
+
+The hot path (per-pixel BVH8 / SDF-grid / SDF-octree intersection and the
+reference's shading) runs in hand-written HIP kernels in librtamd.so; this
+package only marshals arguments.
+"""
+from ._lib import EXPORTED, LIB_PATH, RT_FLAG_CLEAR, RenderParams, RtError, Tile, build, lib
+from .api import (BVHBuilder, Camera, FrameBuffer, HitInfo, IScene, Plane, Renderer, SceneUnion,
+                  SDFGrid, SDFOctree, ShadingMode, SimpleMesh, camera_matrices, device_count,
+                  load_mesh_from_obj, load_sdf_grid, load_sdf_octree, render_params)
+from . import data, workloads
+
+__all__ = [
+    "EXPORTED", "LIB_PATH", "RT_FLAG_CLEAR", "RenderParams", "RtError", "Tile", "build", "lib",
+    "BVHBuilder", "Camera", "FrameBuffer", "HitInfo", "IScene", "Plane", "Renderer", "SceneUnion",
+    "SDFGrid", "SDFOctree", "ShadingMode", "SimpleMesh", "camera_matrices", "device_count",
+    "load_mesh_from_obj", "load_sdf_grid", "load_sdf_octree", "render_params", "data",
+    "workloads",
+]

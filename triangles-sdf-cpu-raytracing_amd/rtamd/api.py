@@ -1,0 +1,318 @@
+"""Python mirror of the reference's render surface, over the C ABI.
+
+Reference interface (iMacsimus/Triangles-SDF-CPU-RayTracing @ 2025-07-04):
+  FrameBuffer {color, t}; clear()             src/raytracing.hpp:9-20
+  ShadingMode {Normal, Lambert, Color}         src/raytracing.hpp:99
+  Renderer {lightPos, enableShadows, enableReflections, shadingMode};
+      float draw(scene, frameBuffer, camera, projInv)  src/raytracing.hpp:101-117
+  IScene::intersect(rayPos, rayDir, tNear, tFar) -> HitInfo  src/raytracing.hpp:75-81
+  BVHBuilder::perform(SimpleMesh)               src/triangles_raytracing.hpp:38-67
+  SDFGrid / loadSDFGrid                         src/grid_raytracing.hpp:10-22
+  SDFOctree / loadSDFOctree                     src/octree_raytracing.hpp:20-49
+  Plane(normal, offset), SceneUnion(a, b)       src/raytracing.hpp:83-97, 119-186
+  Camera(position, target, up)                  src/camera.hpp:7-61
+  cmesh4::LoadMeshFromObj + loadAndScale        src/core/mesh.cpp:178, src/main.cpp:326-343
+
+Every call goes to the HIP implementation in librtamd.so; errors raise RtError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import (RT_FLAG_CLEAR, RenderParams, RtError, Tile, check, lib)
+
+__all__ = [
+    "ShadingMode", "SimpleMesh", "FrameBuffer", "Camera", "Renderer", "HitInfo", "IScene",
+    "BVHBuilder", "SDFGrid", "SDFOctree", "Plane", "SceneUnion", "load_mesh_from_obj",
+    "load_sdf_grid", "load_sdf_octree", "camera_matrices", "render_params", "RtError",
+    "RT_FLAG_CLEAR", "Tile", "device_count",
+]
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def device_count() -> int:
+    return lib().rt_device_count()
+
+
+class ShadingMode(enum.IntEnum):
+    Normal = 0
+    Lambert = 1
+    Color = 2
+
+
+@dataclass
+class SimpleMesh:
+    """cmesh4::SimpleMesh positions + indices (src/core/mesh.h:15-55)."""
+    vPos4f: np.ndarray      # float32 [N, 4]
+    indices: np.ndarray     # uint32 [3*T]
+
+    def TrianglesNum(self) -> int:
+        return len(self.indices) // 3
+
+
+def load_mesh_from_obj(path: str, scale: bool = True) -> SimpleMesh:
+    """LoadMeshFromObj (+ loadAndScale when scale=True, as main.cpp does for every .obj)."""
+    L = lib()
+    nv, ni = C.c_int64(0), C.c_int64(0)
+    check(L.rt_load_obj(path.encode(), int(scale), None, C.byref(nv), None, C.byref(ni)))
+    v = np.empty((nv.value, 4), np.float32)
+    i = np.empty(ni.value, np.uint32)
+    check(L.rt_load_obj(path.encode(), int(scale), _p(v), C.byref(nv), _p(i), C.byref(ni)))
+    return SimpleMesh(v, i)
+
+
+def load_sdf_grid(path: str):
+    """loadSDFGrid -> (size uint32[3], values float32[sx*sy*sz])."""
+    L = lib()
+    size = np.zeros(3, np.uint32)
+    check(L.rt_load_grid(path.encode(), _p(size), None))
+    vals = np.empty(int(size[0]) * int(size[1]) * int(size[2]), np.float32)
+    check(L.rt_load_grid(path.encode(), _p(size), _p(vals)))
+    return size, vals
+
+
+def load_sdf_octree(path: str) -> np.ndarray:
+    """loadSDFOctree -> raw nodes, uint8 [count*36] (SDFOctreeNode, 36 B each)."""
+    L = lib()
+    n = C.c_int64(0)
+    check(L.rt_load_octree(path.encode(), C.byref(n), None))
+    buf = np.empty(n.value * 36, np.uint8)
+    check(L.rt_load_octree(path.encode(), C.byref(n), _p(buf)))
+    return buf
+
+
+def camera_matrices(position, target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0), fovy=45.0,
+                    aspect=16.0 / 9.0, znear=0.01, zfar=100.0):
+    """(view_inv, proj_inv) column-major float32[16]:
+    inverse4x4(Camera(position, target, up).lookAtMatrix()) and
+    inverse4x4(perspectiveMatrix(fovy, aspect, znear, zfar)) (main.cpp:198-201)."""
+    # keep the argument arrays alive across the call (a temporary's buffer may be freed)
+    pos = np.array(position, np.float32)
+    tgt = np.array(target, np.float32)
+    upv = np.array(up, np.float32)
+    vi = np.zeros(16, np.float32)
+    pi = np.zeros(16, np.float32)
+    check(lib().rt_camera(_p(pos), _p(tgt), _p(upv), fovy, aspect, znear, zfar, _p(vi), _p(pi)))
+    return vi, pi
+
+
+def render_params(cam_pos, view_inv, proj_inv, light=(2.0, 2.0, 2.0), mode=ShadingMode.Lambert,
+                  shadows=True, reflections=True) -> RenderParams:
+    P = RenderParams()
+    P.camera_pos[:] = [float(x) for x in cam_pos]
+    P.view_inv[:] = [float(x) for x in view_inv]
+    P.proj_inv[:] = [float(x) for x in proj_inv]
+    P.light_pos[:] = [float(x) for x in light]
+    P.shading_mode = int(mode)
+    P.enable_shadows = int(bool(shadows))
+    P.enable_reflections = int(bool(reflections))
+    P.reserved = 0
+    return P
+
+
+class Camera:
+    """Camera(position, target, up) (src/camera.hpp:7-61): view matrix only."""
+
+    def __init__(self, position, target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)):
+        self._pos = np.asarray(position, np.float32)
+        self._target = np.asarray(target, np.float32)
+        self._up = np.asarray(up, np.float32)
+
+    def position(self):
+        return self._pos.copy()
+
+    def target(self):
+        return self._target.copy()
+
+    def view_inv(self):
+        vi, _ = camera_matrices(self._pos, self._target, self._up)
+        return vi
+
+
+class FrameBuffer:
+    """FrameBuffer {Image2D<uint32_t> color; Image2D<float> t;} (raytracing.hpp:9-20)."""
+
+    def __init__(self, width: int, height: int):
+        self.resize(width, height)
+
+    def resize(self, width: int, height: int):
+        self.color = np.zeros((height, width), np.uint32)
+        self.t = np.full((height, width), np.inf, np.float32)
+
+    def clear(self):
+        self.color.fill(0)
+        self.t.fill(np.inf)
+
+    @property
+    def width(self):
+        return self.color.shape[1]
+
+    @property
+    def height(self):
+        return self.color.shape[0]
+
+
+@dataclass
+class HitInfo:
+    """HitInfo (raytracing.hpp:67-73) for a batch; prim is this build's primitive id."""
+    hitten: np.ndarray
+    t: np.ndarray
+    normal: np.ndarray
+    prim: np.ndarray
+
+
+class IScene:
+    """A scene resident on the current HIP device (one rt_scene handle)."""
+
+    _h = None
+    _plane = None
+
+    def _handle(self):
+        if self._h is None:
+            raise RtError("scene not built")
+        return self._h
+
+    def set_plane(self, plane: "Plane | None"):
+        self._plane = plane
+        if plane is None:
+            check(lib().rt_scene_set_plane(self._handle(), 0, None, 0.0))
+        else:
+            n = np.asarray(plane.normal, np.float32)
+            check(lib().rt_scene_set_plane(self._handle(), 1, _p(n), float(plane.offset)))
+
+    def intersect(self, ray_pos, ray_dir, tNear=0.01, tFar=100.0) -> HitInfo:
+        """IScene::intersect for a batch of rays ([N,3] origins and directions)."""
+        o = np.ascontiguousarray(np.asarray(ray_pos, np.float32).reshape(-1, 3))
+        d = np.ascontiguousarray(np.asarray(ray_dir, np.float32).reshape(-1, 3))
+        n = len(o)
+        hit = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        prim = np.zeros(n, np.int64)
+        check(lib().rt_intersect_rays(self._handle(), _p(o), _p(d), n, tNear, tFar, _p(hit), _p(t),
+                                      _p(nrm), _p(prim)))
+        return HitInfo(hit.astype(bool), t, nrm, prim)
+
+    def render(self, params: RenderParams, color: np.ndarray, t: np.ndarray, clear: bool = False):
+        """Renderer::draw on host buffers; returns the kernel time in ms."""
+        H, W = color.shape
+        assert color.dtype == np.uint32 and t.dtype == np.float32 and t.shape == color.shape
+        assert color.flags.c_contiguous and t.flags.c_contiguous
+        ms = C.c_float(0.0)
+        check(lib().rt_render(self._handle(), C.byref(params), _p(color), _p(t), W, H,
+                              RT_FLAG_CLEAR if clear else 0, C.byref(ms)))
+        return ms.value
+
+    def render_device(self, params: RenderParams, color_ptr: int, t_ptr: int, W: int, H: int,
+                      clear: bool = True, tile: Tile | None = None, stream: int | None = None):
+        """Renderer::draw into device buffers (e.g. torch tensors' data_ptr())."""
+        check(lib().rt_render_device(self._handle(), C.byref(params), C.c_void_p(color_ptr),
+                                     C.c_void_p(t_ptr), W, H, RT_FLAG_CLEAR if clear else 0,
+                                     C.byref(tile) if tile is not None else None,
+                                     C.c_void_p(stream) if stream else None))
+
+    def bench_frames(self, params_list, W: int, H: int, clear: bool = True):
+        arr = (RenderParams * len(params_list))(*params_list)
+        mean, total = C.c_float(0.0), C.c_float(0.0)
+        check(lib().rt_bench_frames(self._handle(), arr, len(params_list), W, H,
+                                    RT_FLAG_CLEAR if clear else 0, C.byref(mean), C.byref(total)))
+        return mean.value, total.value
+
+    def device_bytes(self) -> int:
+        return int(lib().rt_scene_device_bytes(self._handle()))
+
+    def tree_stats(self):
+        n, i, d = C.c_int64(0), C.c_int64(0), C.c_int32(0)
+        check(lib().rt_scene_bvh_stats(self._handle(), C.byref(n), C.byref(i), C.byref(d)))
+        return n.value, i.value, d.value
+
+    def close(self):
+        if self._h is not None:
+            lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BVHBuilder(IScene):
+    """BVHBuilder::perform(mesh): host SAH BVH8 build + device upload."""
+
+    def __init__(self, mesh: SimpleMesh | None = None):
+        if mesh is not None:
+            self.perform(mesh)
+
+    def perform(self, mesh: SimpleMesh):
+        self.close()
+        v = np.ascontiguousarray(mesh.vPos4f, np.float32)
+        i = np.ascontiguousarray(mesh.indices, np.uint32)
+        h = C.c_void_p()
+        check(lib().rt_scene_create_mesh(_p(v), len(v), _p(i), len(i), C.byref(h)))
+        self._h = h
+        return self
+
+
+class SDFGrid(IScene):
+    def __init__(self, size, values):
+        size = np.ascontiguousarray(size, np.uint32)
+        values = np.ascontiguousarray(values, np.float32)
+        h = C.c_void_p()
+        check(lib().rt_scene_create_grid(_p(size), _p(values), C.byref(h)))
+        self._h = h
+        self.size = size
+
+
+class SDFOctree(IScene):
+    def __init__(self, nodes36: np.ndarray):
+        nodes36 = np.ascontiguousarray(nodes36).view(np.uint8)
+        h = C.c_void_p()
+        check(lib().rt_scene_create_octree(_p(nodes36), nodes36.nbytes // 36, C.byref(h)))
+        self._h = h
+
+
+@dataclass
+class Plane:
+    """Plane(normal, offset): the plane dot(p, normal) = offset (raytracing.hpp:121-124)."""
+    normal: tuple = (0.0, 1.0, 0.0)
+    offset: float = 0.0
+
+
+class SceneUnion:
+    """SceneUnion(scene, plane) (raytracing.hpp:83-97). The second operand must be a Plane."""
+
+    def __init__(self, first: IScene, second: Plane):
+        if not isinstance(second, Plane):
+            raise RtError("SceneUnion supports (scene, Plane) as in the reference application")
+        self.first, self.second = first, second
+
+
+class Renderer:
+    """Renderer (raytracing.hpp:101-117)."""
+
+    def __init__(self):
+        self.lightPos = (2.0, 2.0, 2.0)  # main.cpp:60
+        self.enableShadows = True
+        self.enableReflections = True
+        self.shadingMode = ShadingMode.Lambert
+
+    def draw(self, scene, frame_buffer: FrameBuffer, camera: Camera, proj_inv) -> float:
+        """Renderer::draw: renders into frame_buffer (t read as tPrev, written on hit)."""
+        if isinstance(scene, SceneUnion):
+            base = scene.first
+            base.set_plane(scene.second)
+        else:
+            base = scene
+            base.set_plane(None)
+        P = render_params(camera.position(), camera.view_inv(), proj_inv, self.lightPos,
+                          self.shadingMode, self.enableShadows, self.enableReflections)
+        return base.render(P, frame_buffer.color, frame_buffer.t, clear=False)

@@ -1,0 +1,48 @@
+"""Benchmark / test workloads (BASELINE.json configs).
+
+Camera orbit (synthetic, deterministic): frame k of N looks at the origin from
+pos_k = (2.5 sin(2 pi k/N), 0.5, 2.5 cos(2 pi k/N)), up (0,1,0), fovy 45,
+near 0.01, far 100, light (2,2,2); ground plane at the model's bbox min y
+(grid / octree: -1), as main.cpp:189 sets it.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import api, data
+
+DEFAULT_EYE = (0.0, 0.0, 2.5)  # main.cpp:89-91
+
+
+def orbit_positions(n: int = 64, radius: float = 2.5, height: float = 0.5):
+    return [(radius * math.sin(2 * math.pi * k / n), height, radius * math.cos(2 * math.pi * k / n))
+            for k in range(n)]
+
+
+def params_for(pos, W, H, mode=api.ShadingMode.Normal, shadows=True, reflections=True,
+               light=(2.0, 2.0, 2.0)):
+    vi, pi = api.camera_matrices(pos, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 45.0, W / H, 0.01, 100.0)
+    return api.render_params(pos, vi, pi, light, mode, shadows, reflections)
+
+
+def load_input(name: str):
+    """-> (kind, payload, plane_offset). kind in {'mesh','grid','octree'}."""
+    if name.endswith(".obj"):
+        m = api.load_mesh_from_obj(data.path(name), scale=True)
+        return "mesh", m, float(m.vPos4f[:, 1].min() / 1.0)
+    if name.endswith(".grid"):
+        return "grid", api.load_sdf_grid(data.path(name)), -1.0
+    if name.endswith(".octree"):
+        return "octree", api.load_sdf_octree(data.path(name)), -1.0
+    raise ValueError(name)
+
+
+def make_scene(kind: str, payload):
+    if kind == "mesh":
+        return api.BVHBuilder(payload)
+    if kind == "grid":
+        size, vals = payload
+        return api.SDFGrid(size, vals)
+    return api.SDFOctree(payload)
