@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""bench.py -- primary-ray throughput of the MI355X renderer (BASELINE.json metric).
+
+Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355X".
+Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
+1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
+the pure intersection hot path), over a deterministic 64-frame camera orbit
+(SURVEY.md 8(d)). A "step" is one frame. The SDF grid (configs[2] shape, on the
+shipped 65^3 example_grid.grid) is measured the same way and reported under
+"extra" at N=1.
+
+Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every frame is
+split into 16-row bands dealt round-robin to the ranks (load balance: the model
+covers the middle rows); each rank renders its bands packed, then ONE RCCL
+gather per frame brings colour+t (8 B/pixel) to rank 0, which de-interleaves
+them on the device. Gathers are double-buffered so frame k's gather overlaps
+frame k+1's render. Total work per step is fixed (one 1080p frame), so scaling
+is "strong"; value = pixels of all frames / max-over-ranks wall time.
+
+Timing: W untimed warm-up frames, then exactly K frames between barrier +
+torch.cuda.synchronize() on both sides; max over ranks. Inputs are resident
+in HBM before the timed region. Roofline: algorithmic bytes per launch
+(SURVEY.md 8(d) byte model, counted exactly by a diagnostic variant of the
+same kernel over the same frames) / the render kernel's average duration
+(HIP events around each launch on the launch stream); peak 8.0 TB/s HBM.
+cpu_baseline: the oracle (C++ restatement of the reference's CPU path, with
+the ISPC kernels in scalar C++) on the host cores, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd"))
+
+import torch  # noqa: E402  (load torch's HIP runtime first: one runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import rtamd  # noqa: E402
+from rtamd import workloads as WL  # noqa: E402
+
+METRIC = "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+W_IMG, H_IMG = 1920, 1080
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--workload", default="stanford-bunny.obj")
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
+    return ap.parse_args()
+
+
+def host_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def frame_params(n_frames):
+    orbit = WL.orbit_positions(64)
+    return [WL.params_for(orbit[k % 64], W_IMG, H_IMG, rtamd.ShadingMode.Normal)
+            for k in range(n_frames)]
+
+
+def run_single(scene, params, warmup, steps):
+    """N=1: full frames, render kernel only. Returns (wall_s, kernel_ms_avg)."""
+    dev = torch.device("cuda")
+    color = torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev)
+    tbuf = torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev)
+    for k in range(warmup):
+        scene.render_device(params[k], color.data_ptr(), tbuf.data_ptr(), W_IMG, H_IMG, clear=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        evs[k][0].record()
+        scene.render_device(params[warmup + k], color.data_ptr(), tbuf.data_ptr(), W_IMG, H_IMG,
+                            clear=True)
+        evs[k][1].record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    return wall, kms, (color, tbuf)
+
+
+def run_distributed(scene, params, warmup, steps, rank, world, band):
+    """N>1: row bands per rank + one RCCL gather per frame to rank 0."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    tiles = [rtamd.Tile(band, r, world, 0) for r in range(world)]
+    per = max(rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(t)) for t in tiles)
+    # packed slot: [colour (per) | t (per)] as int32 words, double-buffered; rank 0
+    # gathers straight into rank-major rows of one [world, 2*per] buffer per slot
+    bufs = [torch.zeros(2 * per, dtype=torch.int32, device=dev) for _ in range(2)]
+    stacked = ([torch.empty((world, 2 * per), dtype=torch.int32, device=dev) for _ in range(2)]
+               if rank == 0 else None)
+    recv = [list(stacked[s].unbind(0)) for s in range(2)] if rank == 0 else None
+    frame_c = torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev) if rank == 0 else None
+    frame_t = torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev) if rank == 0 else None
+    tile = tiles[rank]
+    ev = []
+
+    def untile(slot):
+        # rank r's colour words start at r*(2*per), its t words per words later
+        base = stacked[slot].data_ptr()
+        rtamd._lib.check(rtamd.lib().rt_untile_device(
+            ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * per), 2 * per,
+            ctypes.c_void_p(frame_c.data_ptr()), ctypes.c_void_p(frame_t.data_ptr()), W_IMG, H_IMG,
+            ctypes.byref(tiles[0]), None))
+
+    def step(k, timed):
+        slot = k & 1
+        b = bufs[slot]
+        if pending[slot] is not None:
+            pending[slot].wait()
+            if rank == 0:
+                untile(slot)
+            pending[slot] = None
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        scene.render_device(params[k], b.data_ptr(), b.data_ptr() + 4 * per, W_IMG, H_IMG,
+                            clear=True, tile=tile)
+        if timed:
+            e1.record()
+            ev.append((e0, e1))
+        pending[slot] = dist.gather(b, gather_list=recv[slot] if rank == 0 else None, dst=0,
+                                    async_op=True)
+
+    def drain():
+        for slot in (0, 1):
+            if pending[slot] is not None:
+                pending[slot].wait()
+                if rank == 0:
+                    untile(slot)
+                pending[slot] = None
+
+    pending = [None, None]
+    for k in range(warmup):
+        step(k, False)
+    drain()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k, True)
+    drain()
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    kms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    return wall, kms, tile
+
+
+def roofline(scene, params, tile, kms):
+    c = scene.count_work(params, W_IMG, H_IMG, clear=True, tile=tile)
+    npx = (rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(tile))
+           if tile is not None else W_IMG * H_IMG)
+    algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params)
+    achieved = algo / (kms * 1e-3) / 1e9
+    per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
+            "work_per_ray": per_ray}
+
+
+def cpu_baseline(name, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpuref  # the oracle: test infrastructure, used here only as the CPU baseline
+    from rtamd import data
+    p = data.path(name)
+    threads = host_threads()
+    if name.endswith(".obj"):
+        v, i = cpuref.load_obj(p)
+        sc = cpuref.RefScene.mesh(v, i)
+    else:
+        import numpy as np
+        size = np.fromfile(p, np.uint32, 3)
+        vals = np.fromfile(p, np.float32, offset=12)
+        sc = cpuref.RefScene.grid(size, vals)
+    sc.set_plane(False)
+    orbit = WL.orbit_positions(64)
+    frames, ms_total = 0, 0.0
+    t0 = time.perf_counter()
+    while frames < 64 and (time.perf_counter() - t0) < budget_s:
+        vi, pi = cpuref.camera_matrices(orbit[frames], aspect=W_IMG / H_IMG)
+        P = cpuref.make_params(orbit[frames], vi, pi, mode=0)
+        _, _, _, ms = sc.render(P, W_IMG, H_IMG, threads=threads)
+        ms_total += ms
+        frames += 1
+    mrays = W_IMG * H_IMG * frames / (ms_total * 1e-3) / 1e6
+    return {"value": round(mrays, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "ms_per_frame": round(ms_total / frames, 2),
+            "sample": f"{frames} frames of the 64-frame orbit, {name} {W_IMG}x{H_IMG} primary rays, "
+                      f"OpenMP schedule(dynamic) over rows, {threads} threads, ISPC kernels as scalar "
+                      f"C++ (oracle/cpuref.cpp)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rtamd.lib().rt_set_device(local)
+
+    kind, payload, _ = WL.load_input(a.workload)
+    scene = WL.make_scene(kind, payload)
+    scene.set_plane(None)
+    params = frame_params(a.warmup + a.steps)
+
+    if world == 1:
+        wall, kms, _ = run_single(scene, params, a.warmup, a.steps)
+        tile = None
+    else:
+        wall, kms, tile = run_distributed(scene, params, a.warmup, a.steps, rank, world, a.band_rows)
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    rl = roofline(scene, params[a.warmup:], tile, kms)
+    total_rays = W_IMG * H_IMG * a.steps
+    value = total_rays / wall / 1e6
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic deterministic 64-frame camera orbit over the shipped {a.workload}",
+        "config": {"workload": f"{a.workload} triangles {W_IMG}x{H_IMG} primary rays "
+                               "(BASELINE configs[1]); Normal shading, no plane",
+                   "resolution": [W_IMG, H_IMG], "camera": "orbit r=2.5 h=0.5 fovy 45",
+                   "parallelism": f"row bands of {a.band_rows} rows x {world} GPUs + RCCL gather"
+                   if world > 1 else "1 GPU, 1 thread per pixel"},
+        "roofline": rl,
+    }
+    if rank == 0 and world == 1 and not a.no_extra:
+        gkind, gpayload, _ = WL.load_input("example_grid.grid")
+        g = WL.make_scene(gkind, gpayload)
+        g.set_plane(None)
+        gwall, gkms, _ = run_single(g, params, a.warmup, a.steps)
+        out["extra"] = {"grid": {
+            "workload": "example_grid.grid (65^3, shipped stand-in for example_grid_large) "
+                        f"{W_IMG}x{H_IMG} primary rays",
+            "value": round(total_rays / gwall / 1e6, 1), "unit": "Mrays/s",
+            "ms_per_step": round(gwall * 1e3 / a.steps, 4),
+            "roofline": roofline(g, params[a.warmup:], None, gkms)}}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

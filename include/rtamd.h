@@ -166,6 +166,16 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
 int rt_bench_frames(rt_scene *s, const rt_render_params *params, int32_t frames, int32_t W,
                     int32_t H, uint32_t flags, float *mean_ms, float *total_ms);
 
+/* Work counters of the reference traversal for `frames` frames (diagnostic
+ * kernel variant; same traversal as the timed kernels): counters[0..8] =
+ * BVH inner-node visits, BVH leaf visits, triangle tests, grid sdf
+ * evaluations, octree node visits, octree leaf visits, octree march steps,
+ * octree normal evaluations, rays (scene intersections). Shadow rays stop at
+ * their first hit here, so with shadows on the counts are lower than the
+ * reference's full traversal; primary-ray counts are identical. */
+int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, int32_t W, int32_t H,
+                  uint32_t flags, const rt_tile *tile, int64_t counters[9]);
+
 #ifdef __cplusplus
 }
 #endif

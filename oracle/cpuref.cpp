@@ -50,6 +50,16 @@ namespace ref {
 
 static const float INF = std::numeric_limits<float>::infinity();
 
+// Work counters for the algorithmic-bytes model of SURVEY.md 8(d) (oracle
+// bookkeeping only; they do not influence any result).
+struct Counters {
+  long long bvh_inner = 0, bvh_leaf = 0, bvh_tri = 0;   // traverseNode calls / triangle tests
+  long long grid_sdf = 0;                               // SDFGrid::sdf(float3) evaluations
+  long long oct_node = 0, oct_leaf = 0, oct_step = 0, oct_normal = 0;
+  long long rays = 0;                                   // scene.intersect calls
+};
+static thread_local Counters tl_cnt;
+
 // ---------------------------------------------------------------- L0 math --
 // LiteMath restatement (SURVEY 8(c) "Shim formulas").
 struct float3 {
@@ -552,6 +562,7 @@ struct BVHBuilder final : IScene {
   HitInfo traverseNode(size_t index, float3 o, float3 d, float tNear, float tFar) const {
     const BVH8Node &node = nodes[index];
     HitInfo result;
+    if (!node.isLeaf) tl_cnt.bvh_inner++; else tl_cnt.bvh_leaf++;
     if (!node.isLeaf) {
       float t[8] = {};
       float3 inv = 1.0f / d;  // triangles_raytracing.cpp:273
@@ -568,6 +579,7 @@ struct BVHBuilder final : IScene {
     } else {
       uint32_t start = node.startIndex, end = start + node.count;
       uint32_t ntri = std::min((end - start) / 3, 8u);
+      tl_cnt.bvh_tri += ntri;
       for (uint32_t k = 0; k < ntri; ++k) {
         float4 v0 = mesh.vPos4f[mesh.indices[start + k * 3]];
         float4 v1 = mesh.vPos4f[mesh.indices[start + k * 3 + 1]];
@@ -596,6 +608,7 @@ struct SDFGrid final : IScene {  // grid_raytracing.hpp:10-21
   float at(uint32_t x, uint32_t y, uint32_t z) const { return values[(x * sy + y) * sz + z]; }
   // grid_raytracing.cpp:7-62
   float sdf(float3 p, int64_t *cell = nullptr) const {
+    tl_cnt.grid_sdf++;
     p = (p + 1.0f) / 2.0f;
     p = p * float3((float)(sx - 1), (float)(sy - 1), (float)(sz - 1));
     float3 c0f = vfloor(p), c1f = vceil(p);
@@ -670,6 +683,7 @@ struct SDFOctree final : IScene {
   }
   // octree_raytracing.cpp:18-57
   float nodeSDF(size_t id, const BBox3f &box, float3 p) const {
+    tl_cnt.oct_step++;
     p = (p - box.boxMin) / (box.boxMax - box.boxMin);
     p = vmin(vmax(p, float3(0.0000001f)), float3(0.9999999f));
     float3 c0f = vfloor(p), c1f = vceil(p);
@@ -693,6 +707,7 @@ struct SDFOctree final : IScene {
   }
   // octree_raytracing.cpp:60-118
   float3 nodeNormal(size_t id, const BBox3f &box, float3 p) const {
+    tl_cnt.oct_normal++;
     p = (p - box.boxMin) / (box.boxMax - box.boxMin);
     p = vmin(vmax(p, float3(0.0000001f)), float3(0.9999999f));
     float3 c0f = vfloor(p), c1f = vceil(p);
@@ -718,6 +733,7 @@ struct SDFOctree final : IScene {
   // octree_raytracing.cpp:122-164
   HitInfo intersectLeaf(size_t id, const BBox3f &box, float3 o, float3 d, float tNear, float tFar) const {
     HitInfo res;
+    tl_cnt.oct_leaf++;
     const OctNode &n = nodes[id];
     if (isEmpty(n)) return res;
     bool allAbove = true;
@@ -748,6 +764,7 @@ struct SDFOctree final : IScene {
   // octree_raytracing.cpp:166-202
   HitInfo intersectNode(size_t id, float3 o, float3 d, float tNear, float tFar, const BBox3f &box) const {
     const OctNode &node = nodes[id];
+    tl_cnt.oct_node++;
     if (node.childrenOffset == 0) return intersectLeaf(id, box, o, d, tNear, tFar);
     Box8 b8;
     divide_box_8(box.boxMin, box.boxMax, b8);
@@ -790,6 +807,7 @@ struct Renderer {
   // raytracing.cpp:13-65
   std::pair<float4, float> color(const IScene &scene, float3 o, float3 d, float tNear, float tFar,
                                  float tPrev, int maxDepth, int64_t *prim) const {
+    tl_cnt.rays++;
     HitInfo hit = scene.intersect(o, d, tNear, std::min(tFar, tPrev));
     if (prim) *prim = hit.hitten ? hit.prim : -1;
     if (!hit.hitten) return {float4(0.0f, 0.0f, 0.0f, 1.0f), INF};
@@ -805,6 +823,7 @@ struct Renderer {
       float3 point = o + hit.t * d;
       if (enableShadows) {
         float3 sd = normalize(lightPos - point);
+        tl_cnt.rays++;
         HitInfo sh = scene.intersect(point + 0.3f * sd, sd, 0.01f, 100.0f);
         visible = !sh.hitten;
       }
@@ -950,7 +969,21 @@ struct RefParams {
   int32_t reserved;
 };
 
+static Counters g_cnt;
+
 extern "C" {
+
+// Work counters accumulated by cpuref_render since the last reset:
+// out[0..8] = bvh_inner, bvh_leaf, bvh_tri, grid_sdf, oct_node, oct_leaf,
+//             oct_step, oct_normal, rays.
+void cpuref_counters(int reset, int64_t *out) {
+  if (out) {
+    out[0] = g_cnt.bvh_inner; out[1] = g_cnt.bvh_leaf; out[2] = g_cnt.bvh_tri; out[3] = g_cnt.grid_sdf;
+    out[4] = g_cnt.oct_node; out[5] = g_cnt.oct_leaf; out[6] = g_cnt.oct_step; out[7] = g_cnt.oct_normal;
+    out[8] = g_cnt.rays;
+  }
+  if (reset) g_cnt = Counters();
+}
 
 void *cpuref_load_obj(const char *path, int scale, int64_t *nverts, int64_t *nidx) {
   Mesh *m = new Mesh();
@@ -1060,7 +1093,10 @@ double cpuref_render(void *h, const RefParams *P, uint32_t *color, float *tbuf, 
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
   auto b = std::chrono::high_resolution_clock::now();
-#pragma omp parallel for schedule(dynamic)
+#pragma omp parallel
+  {
+  tl_cnt = Counters();
+#pragma omp for schedule(dynamic)
   for (int yo = row0; yo < row1; ++yo) {
     int y = H - yo - 1;  // loop row y stores to image row H-y-1 (raytracing.cpp:82)
     for (int x = 0; x < W; ++x) {
@@ -1077,6 +1113,13 @@ double cpuref_render(void *h, const RefParams *P, uint32_t *color, float *tbuf, 
         color[xy] = color_pack_rgba(res.first);
       }
     }
+  }
+#pragma omp critical(cpuref_counters)
+  {
+    g_cnt.bvh_inner += tl_cnt.bvh_inner; g_cnt.bvh_leaf += tl_cnt.bvh_leaf; g_cnt.bvh_tri += tl_cnt.bvh_tri;
+    g_cnt.grid_sdf += tl_cnt.grid_sdf; g_cnt.oct_node += tl_cnt.oct_node; g_cnt.oct_leaf += tl_cnt.oct_leaf;
+    g_cnt.oct_step += tl_cnt.oct_step; g_cnt.oct_normal += tl_cnt.oct_normal; g_cnt.rays += tl_cnt.rays;
+  }
   }
   auto e = std::chrono::high_resolution_clock::now();
   (void)rays;

@@ -54,6 +54,7 @@ def lib():
         L.cpuref_render.restype = f64
         L.cpuref_render.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
         L.cpuref_intersect_rays.argtypes = [vp, vp, vp, i64, f32, f32, vp, vp, vp, vp]
+        L.cpuref_counters.argtypes = [C.c_int, vp]
         L.cpuref_fnv1a64.restype = C.c_uint64
         L.cpuref_fnv1a64.argtypes = [vp, i64]
         _lib = L
@@ -188,3 +189,24 @@ def fnv1a64_words(color: np.ndarray) -> str:
     """Word-wise FNV-1a-64 over the colour buffer in y*W+x order."""
     c = np.ascontiguousarray(color, np.uint32).ravel()
     return f"{lib().cpuref_fnv1a64(_p(c), c.size):016x}"
+
+
+COUNTER_NAMES = ("bvh_inner", "bvh_leaf", "bvh_tri", "grid_sdf", "oct_node", "oct_leaf", "oct_step",
+                 "oct_normal", "rays")
+
+
+def counters(reset: bool = True) -> dict:
+    """Work counters of cpuref_render calls since the last reset (SURVEY 8(d) byte model)."""
+    out = np.zeros(len(COUNTER_NAMES), np.int64)
+    lib().cpuref_counters(int(reset), _p(out))
+    return dict(zip(COUNTER_NAMES, out.tolist()))
+
+
+def algorithmic_bytes(c: dict, pixels: int) -> int:
+    """Bytes the reference's data layout makes one frame touch:
+    BVH: 200 B / inner node visit, 8 B / leaf visit, 60 B / triangle test;
+    grid: 32 B / sdf evaluation; octree: 4 B / node visit, 32 B / leaf visit,
+    32 B / nodeSDF step, 32 B / nodeNormal; + 8 B / pixel framebuffer (colour + t)."""
+    return int(200 * c["bvh_inner"] + 8 * c["bvh_leaf"] + 60 * c["bvh_tri"] + 32 * c["grid_sdf"]
+               + 4 * c["oct_node"] + 32 * c["oct_leaf"] + 32 * c["oct_step"] + 32 * c["oct_normal"]
+               + 8 * pixels)

@@ -50,35 +50,41 @@ struct FrameArgs {
 // ---------------------------------------------------------- scene adapters --
 struct MeshS {
   MeshDev d;
-  template <int B>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
-    return mesh_intersect<B>(d, o, dir, tn, tf, st);
+  template <int B, class CT>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
+                                           CT &cnt) const {
+    return mesh_intersect<B>(d, o, dir, tn, tf, st, cnt);
   }
-  template <int B>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
-    return mesh_occluded<B>(d, o, dir, tn, tf, st);
+  template <int B, class CT>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
+                                           CT &cnt) const {
+    return mesh_occluded<B>(d, o, dir, tn, tf, st, cnt);
   }
 };
 struct GridS {
   GridDev d;
-  template <int B>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B>) const {
-    return grid_intersect(d, o, dir, tn, tf);
+  template <int B, class CT>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B>,
+                                           CT &cnt) const {
+    return grid_intersect(d, o, dir, tn, tf, cnt);
   }
-  template <int B>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B>) const {
-    return grid_occluded(d, o, dir, tn, tf);
+  template <int B, class CT>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B>,
+                                           CT &cnt) const {
+    return grid_occluded(d, o, dir, tn, tf, cnt);
   }
 };
 struct OctS {
   OctDev d;
-  template <int B>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
-    return oct_intersect<B>(d, o, dir, tn, tf, st);
+  template <int B, class CT>
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
+                                           CT &cnt) const {
+    return oct_intersect<B>(d, o, dir, tn, tf, st, cnt);
   }
-  template <int B>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st) const {
-    return oct_occluded<B>(d, o, dir, tn, tf, st);
+  template <int B, class CT>
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
+                                           CT &cnt) const {
+    return oct_occluded<B>(d, o, dir, tn, tf, st, cnt);
   }
 };
 
@@ -89,10 +95,11 @@ struct SurfHit {
   float albedo;   // grey albedo: mesh/SDF 1.0, plane checker 0.0 / 1.0
   float refl;     // reflectiveness: plane 0.3, else 0
 };
-template <class S, int B>
+template <class S, int B, class CT>
 __device__ __forceinline__ SurfHit union_intersect(const S &sc, const PlaneDev &pl, f3 o, f3 d,
-                                                   float tn, float tf, LdsStack<B> st) {
-  SurfHit r{sc.template intersect<B>(o, d, tn, tf, st), 1.0f, 0.0f};
+                                                   float tn, float tf, LdsStack<B> st, CT &cnt) {
+  cnt.add(C_RAYS, 1);
+  SurfHit r{sc.template intersect<B>(o, d, tn, tf, st, cnt), 1.0f, 0.0f};
   if (pl.on) {
     float tp = kInf, ap = 1.0f;
     const bool ph = plane_hit(pl, o, d, tn, tf, tp, ap);
@@ -111,10 +118,11 @@ __device__ __forceinline__ SurfHit union_intersect(const S &sc, const PlaneDev &
   return r;
 }
 // Shadow query: HitInfo::hitten of the union is the OR of both hitten flags.
-template <class S, int B>
+template <class S, int B, class CT>
 __device__ __forceinline__ bool union_occluded(const S &sc, const PlaneDev &pl, f3 o, f3 d, float tn,
-                                               float tf, LdsStack<B> st) {
-  if (sc.template occluded<B>(o, d, tn, tf, st)) return true;
+                                               float tf, LdsStack<B> st, CT &cnt) {
+  cnt.add(C_RAYS, 1);
+  if (sc.template occluded<B>(o, d, tn, tf, st, cnt)) return true;
   if (pl.on) {
     float tp, ap;
     return plane_hit(pl, o, d, tn, tf, tp, ap);
@@ -124,21 +132,16 @@ __device__ __forceinline__ bool union_occluded(const S &sc, const PlaneDev &pl, 
 
 // Renderer::intersectionColor (raytracing.cpp:13-65) for one ray; the one
 // reflection bounce (maxDepth 2 -> 1) is expanded in place, no recursion.
-template <class S, int B>
-__device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const rt_render_params &P,
-                                        f3 o, f3 d, float tFarEff, bool allow_refl, bool &hit,
-                                        float &t_out, LdsStack<B> st, int64_t *prim);
-
-template <class S, int B>
+template <class S, int B, class CT>
 __device__ __forceinline__ f4 lambert_color(const S &sc, const PlaneDev &pl,
                                             const rt_render_params &P, f3 o, f3 d,
-                                            const SurfHit &sh, f3 n, LdsStack<B> st) {
+                                            const SurfHit &sh, f3 n, LdsStack<B> st, CT &cnt) {
   bool visible = true;
   const f3 point = o + sh.h.t * d;
   const f3 L{P.light_pos[0], P.light_pos[1], P.light_pos[2]};
   if (P.enable_shadows) {
     const f3 sd = normalize(L - point);
-    visible = !union_occluded<S, B>(sc, pl, point + 0.3f * sd, sd, 0.01f, 100.0f, st);
+    visible = !union_occluded<S, B>(sc, pl, point + 0.3f * sd, sd, 0.01f, 100.0f, st, cnt);
   }
   const float a = sh.albedo;
   if (!visible) return f4{a * 0.1f, a * 0.1f, a * 0.1f, 1.0f};
@@ -148,11 +151,11 @@ __device__ __forceinline__ f4 lambert_color(const S &sc, const PlaneDev &pl,
   return f4{std_min(c.x, 1.0f), std_min(c.y, 1.0f), std_min(c.z, 1.0f), 1.0f};
 }
 
-template <class S, int B>
+template <class S, int B, class CT>
 __device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const rt_render_params &P,
                                         f3 o, f3 d, float tFarEff, bool allow_refl, bool &hit,
-                                        float &t_out, LdsStack<B> st, int64_t *prim) {
-  const SurfHit sh = union_intersect<S, B>(sc, pl, o, d, 0.01f, tFarEff, st);
+                                        float &t_out, LdsStack<B> st, int64_t *prim, CT &cnt) {
+  const SurfHit sh = union_intersect<S, B>(sc, pl, o, d, 0.01f, tFarEff, st, cnt);
   if (prim) *prim = sh.h.hit ? sh.h.prim : -1;
   if (!sh.h.hit) {
     hit = false;
@@ -169,18 +172,18 @@ __device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const r
   } else if (P.shading_mode == RT_SHADING_COLOR) {
     c = f4{sh.albedo, sh.albedo, sh.albedo, 1.0f};
   } else {
-    c = lambert_color<S, B>(sc, pl, P, o, d, sh, n, st);
+    c = lambert_color<S, B>(sc, pl, P, o, d, sh, n, st, cnt);
     if (allow_refl && P.enable_reflections && sh.refl > 0.0f) {
       const float dn = dot(d, n);
       const f3 R = normalize(n * dn * (-2.0f) + d);  // LiteMath reflect(dir, normal)
       const f3 point = o + sh.h.t * d;
       // recursive call with maxDepth 1, tPrev = +inf (raytracing.cpp:51-61)
-      const SurfHit rh = union_intersect<S, B>(sc, pl, point + 0.02f * R, R, 0.01f, 100.0f, st);
+      const SurfHit rh = union_intersect<S, B>(sc, pl, point + 0.02f * R, R, 0.01f, 100.0f, st, cnt);
       f4 rc{0.0f, 0.0f, 0.0f, 1.0f};
       if (rh.h.hit) {
         f3 rn = rh.h.n;
         if (dot(rn, R) > 0) rn = rn * -1.0f;
-        rc = lambert_color<S, B>(sc, pl, P, point + 0.02f * R, R, rh, rn, st);
+        rc = lambert_color<S, B>(sc, pl, P, point + 0.02f * R, R, rh, rn, st, cnt);
       }
       const float r = sh.refl, k = 1.0f - sh.refl;
       c = f4{c.x * k + r * rc.x, c.y * k + r * rc.y, c.z * k + r * rc.z, c.w * k + r * rc.w};
@@ -198,44 +201,69 @@ __device__ __forceinline__ int image_row(int yl, const FrameArgs &fa) {
 // Renderer::draw (raytracing.cpp:67-102). GENERAL=false is the primary-ray
 // path (Normal shading, no plane, no secondary rays) used by the headline
 // benchmark; GENERAL=true runs intersectionColor in full.
-template <class S, int MAXD, bool GENERAL>
-__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa) {
+// COUNT=true is a diagnostic variant that also accumulates the work counters
+// (algorithmic-bytes model) into counters[C_NUM]; the timed kernels use COUNT=false.
+template <bool COUNT>
+struct CntSel { using T = NoCnt; };
+template <>
+struct CntSel<true> { using T = LaneCnt; };
+
+__device__ __forceinline__ void flush_counts(NoCnt &, unsigned long long *) {}
+__device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out) {
+#pragma unroll
+  for (int i = 0; i < C_NUM; ++i) {
+    unsigned long long v = c.v[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out + i, v);
+  }
+}
+
+template <class S, int MAXD, bool GENERAL, bool COUNT>
+__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
+                                                        unsigned long long *counters) {
   __shared__ uint32_t stk[MAXD * 3 * kBlock];
+  typename CntSel<COUNT>::T cnt{};
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
   const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
-  if (xo >= fa.W || yl >= fa.rows_local) return;
-  LdsStack<kBlock> st{stk + threadIdx.x};
-  const int yo = image_row(yl, fa);
-  const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
-  const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
-  const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
-  const size_t idx = (size_t)yl * fa.W + xo;
-  const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
-  const float tPrev = clear ? kInf : fa.t[idx];
-  const float tFarEff = std_min(100.0f, tPrev);  // std::min(tFar, tPrev)
-  bool hit;
-  float t;
-  f4 c;
-  if (!GENERAL) {
-    const Hit h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st);
-    hit = h.hit;
-    t = h.t;
-    f3 n = h.n;
-    if (dot(n, d) > 0) n = n * -1.0f;
-    c = f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
-  } else {
-    c = shade_one<S, kBlock>(sc, pl, fa.P, o, d, tFarEff, true, hit, t, st, nullptr);
+  const bool active = xo < fa.W && yl < fa.rows_local;
+  if (!COUNT && !active) return;
+  if (active) {  // (the counting variant keeps every lane for its wave reduction)
+    LdsStack<kBlock> st{stk + threadIdx.x};
+    const int yo = image_row(yl, fa);
+    const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
+    const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
+    const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+    const size_t idx = (size_t)yl * fa.W + xo;
+    const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
+    const float tPrev = clear ? kInf : fa.t[idx];
+    const float tFarEff = std_min(100.0f, tPrev);  // std::min(tFar, tPrev)
+    bool hit;
+    float t;
+    f4 c;
+    if (!GENERAL) {
+      cnt.add(C_RAYS, 1);
+      const Hit h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st, cnt);
+      hit = h.hit;
+      t = h.t;
+      f3 n = h.n;
+      if (dot(n, d) > 0) n = n * -1.0f;
+      c = f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
+    } else {
+      c = shade_one<S, kBlock>(sc, pl, fa.P, o, d, tFarEff, true, hit, t, st, nullptr, cnt);
+    }
+    // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
+    const bool store = hit && !__builtin_isinf(t);
+    if (clear) {
+      fa.color[idx] = store ? pack_rgba(c) : 0u;
+      fa.t[idx] = store ? t : kInf;
+    } else if (store) {
+      fa.color[idx] = pack_rgba(c);
+      fa.t[idx] = t;
+    }
   }
-  // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
-  const bool store = hit && !__builtin_isinf(t);
-  if (clear) {
-    fa.color[idx] = store ? pack_rgba(c) : 0u;
-    fa.t[idx] = store ? t : kInf;
-  } else if (store) {
-    fa.color[idx] = pack_rgba(c);
-    fa.t[idx] = t;
-  }
+  flush_counts(cnt, counters);
 }
 
 // IScene::intersect over a batch of rays (union with the plane if enabled).
@@ -250,7 +278,8 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const f
   LdsStack<kBlock> st{stk + threadIdx.x};
   const f3 o{o3[3 * i], o3[3 * i + 1], o3[3 * i + 2]};
   const f3 d{d3[3 * i], d3[3 * i + 1], d3[3 * i + 2]};
-  const SurfHit sh = union_intersect<S, kBlock>(sc, pl, o, d, tn, tf, st);
+  NoCnt cnt;
+  const SurfHit sh = union_intersect<S, kBlock>(sc, pl, o, d, tn, tf, st, cnt);
   hit[i] = sh.h.hit ? 1 : 0;
   t[i] = sh.h.t;
   nrm[3 * i] = sh.h.n.x;
@@ -330,32 +359,40 @@ int ensure_fb(rt_scene *s, size_t px) {
 
 template <class S, int MAXD>
 void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool general,
-                     hipStream_t stream) {
+                     hipStream_t stream, unsigned long long *counters) {
   const dim3 grid((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
-  if (general)
-    render_kernel<S, MAXD, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa);
-  else
-    render_kernel<S, MAXD, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa);
+  if (counters) {
+    if (general)
+      render_kernel<S, MAXD, true, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+    else
+      render_kernel<S, MAXD, false, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+  } else {
+    if (general)
+      render_kernel<S, MAXD, true, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+    else
+      render_kernel<S, MAXD, false, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+  }
 }
 
-int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
+int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream,
+                  unsigned long long *counters = nullptr) {
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
   if (s->kind == RT_SCENE_MESH) {
     MeshS sc{MeshDev{s->d_nodes, s->d_tris, s->root}};
     switch (s->maxd) {
-      case 8: launch_render_t<MeshS, 8>(sc, s->plane, fa, general, stream); break;
-      case 16: launch_render_t<MeshS, 16>(sc, s->plane, fa, general, stream); break;
-      default: launch_render_t<MeshS, 32>(sc, s->plane, fa, general, stream); break;
+      case 8: launch_render_t<MeshS, 8>(sc, s->plane, fa, general, stream, counters); break;
+      case 16: launch_render_t<MeshS, 16>(sc, s->plane, fa, general, stream, counters); break;
+      default: launch_render_t<MeshS, 32>(sc, s->plane, fa, general, stream, counters); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
     GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
-    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream);
+    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream, counters);
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
-      case 8: launch_render_t<OctS, 8>(sc, s->plane, fa, general, stream); break;
-      case 16: launch_render_t<OctS, 16>(sc, s->plane, fa, general, stream); break;
-      default: launch_render_t<OctS, 32>(sc, s->plane, fa, general, stream); break;
+      case 8: launch_render_t<OctS, 8>(sc, s->plane, fa, general, stream, counters); break;
+      case 16: launch_render_t<OctS, 16>(sc, s->plane, fa, general, stream, counters); break;
+      default: launch_render_t<OctS, 32>(sc, s->plane, fa, general, stream, counters); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
@@ -737,6 +774,32 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
   } while (0);
   cleanup();
   if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rt_intersect_rays: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, int32_t W, int32_t H,
+                  uint32_t flags, const rt_tile *tile, int64_t counters[9]) {
+  if (!s || !params || frames <= 0 || !counters) return set_err(RT_E_INVALID, "bad arguments");
+  int rc = check_params(params, W, H);
+  if (rc) return rc;
+  const size_t px = (size_t)W * H;
+  if ((rc = ensure_fb(s, px))) return rc;
+  unsigned long long *d = nullptr;
+  HIP_TRY(hipMalloc(&d, C_NUM * sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, C_NUM * sizeof(unsigned long long));
+  if (e == hipSuccess) (void)hipMemset(s->d_t, 0x7f, px * 4);
+  for (int32_t f = 0; f < frames && e == hipSuccess && rc == RT_OK; ++f) {
+    FrameArgs fa;
+    if (!(rc = check_params(params + f, W, H)) &&
+        !(rc = fill_frame(fa, params + f, s->d_color, s->d_t, W, H, flags, tile)))
+      rc = launch_render(s, fa, 0, d);
+  }
+  unsigned long long h[C_NUM] = {};
+  if (e == hipSuccess && rc == RT_OK) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (rc) return rc;
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rt_count_work: ") + hipGetErrorString(e));
+  for (int i = 0; i < C_NUM; ++i) counters[i] = (int64_t)h[i];
   return RT_OK;
 }
 

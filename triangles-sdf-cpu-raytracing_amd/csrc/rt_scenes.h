@@ -12,6 +12,20 @@
 
 namespace rtd {
 
+// Work counters (compile-time optional). Index map = oracle's cpuref_counters:
+// 0 bvh_inner 1 bvh_leaf 2 bvh_tri 3 grid_sdf 4 oct_node 5 oct_leaf 6 oct_step
+// 7 oct_normal 8 rays. NoCnt compiles away; LaneCnt is used only by the
+// counting kernel variant that feeds the algorithmic-bytes model.
+enum { C_BVH_INNER = 0, C_BVH_LEAF, C_BVH_TRI, C_GRID_SDF, C_OCT_NODE, C_OCT_LEAF, C_OCT_STEP,
+       C_OCT_NORMAL, C_RAYS, C_NUM };
+struct NoCnt {
+  __device__ __forceinline__ void add(int, uint32_t) {}
+};
+struct LaneCnt {
+  uint32_t v[C_NUM];
+  __device__ __forceinline__ void add(int i, uint32_t n) { v[i] += n; }
+};
+
 struct Hit {
   bool hit;
   float t;
@@ -66,10 +80,13 @@ __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uin
 }
 
 // One leaf: its local best (first wins among equal t, triangle order).
+template <class CT>
 __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, uint32_t w, f3 o,
-                                          f3 d, float &lt, uint32_t &lk) {
+                                          f3 d, float &lt, uint32_t &lk, CT &cnt) {
   const uint32_t first = (w >> 3) & rtl::kMaxLeafFirstTri;
   const uint32_t n = (w & 7u) + 1u;
+  cnt.add(C_BVH_LEAF, 1);
+  cnt.add(C_BVH_TRI, n);
   for (uint32_t k = 0; k < n; ++k) tri_test(tris, first + k, o, d, lt, lk);
 }
 
@@ -116,9 +133,10 @@ struct LdsStack {
 };
 
 // ANY = true: shadow-ray query, stop at the first leaf hit (only hitten is used).
-template <int BLOCK, bool ANY>
+template <int BLOCK, bool ANY, class CT>
 __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                           LdsStack<BLOCK> st, float &out_t, uint32_t &out_k) {
+                                           LdsStack<BLOCK> st, float &out_t, uint32_t &out_k,
+                                           CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
   float gbest = kInf;
   uint32_t gk = rtl::kInvalidChild;
@@ -134,7 +152,7 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
       if (word & rtl::kLeafBit) {
         float lt = kInf;
         uint32_t lk = rtl::kInvalidChild;
-        leaf_test(sc.tris, word, o, d, lt, lk);
+        leaf_test(sc.tris, word, o, d, lt, lk, cnt);
         if (lk != rtl::kInvalidChild) {
           if (ANY) { out_t = lt; out_k = lk; return true; }
           if (lt < fbest) fbest = lt;
@@ -143,6 +161,7 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
       } else {
         uint32_t l, c;
         float tf;
+        cnt.add(C_BVH_INNER, 1);
         expand_node(sc.nodes + word, o, inv, tNear, tFar, l, c, tf);
         if (c != 0) {
           if (depth >= 1) {
@@ -189,13 +208,13 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
   return gk != rtl::kInvalidChild;
 }
 
-template <int BLOCK>
+template <int BLOCK, class CT>
 __device__ __forceinline__ Hit mesh_intersect(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                              LdsStack<BLOCK> st) {
+                                              LdsStack<BLOCK> st, CT &cnt) {
   float t;
   uint32_t k;
   Hit h = miss_hit();
-  if (mesh_trace<BLOCK, false>(sc, o, d, tNear, tFar, st, t, k)) {
+  if (mesh_trace<BLOCK, false>(sc, o, d, tNear, tFar, st, t, k, cnt)) {
     h.hit = true;
     h.t = t;
     h.n = tri_normal(sc.tris, k);
@@ -203,12 +222,12 @@ __device__ __forceinline__ Hit mesh_intersect(const MeshDev &sc, f3 o, f3 d, flo
   }
   return h;
 }
-template <int BLOCK>
+template <int BLOCK, class CT>
 __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                              LdsStack<BLOCK> st) {
+                                              LdsStack<BLOCK> st, CT &cnt) {
   float t;
   uint32_t k;
-  return mesh_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, t, k);
+  return mesh_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, t, k, cnt);
 }
 
 // ------------------------------------------------------------------- grid --
@@ -219,7 +238,9 @@ struct GridDev {
   uint32_t sx, sy, sz;
 };
 
-__device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell) {
+template <class CT>
+__device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell, CT &cnt) {
+  cnt.add(C_GRID_SDF, 1);
   p = f3{(p.x + 1.0f) / 2.0f, (p.y + 1.0f) / 2.0f, (p.z + 1.0f) / 2.0f};
   p = p * f3{(float)(g.sx - 1), (float)(g.sy - 1), (float)(g.sz - 1)};
   const float c0x = __builtin_floorf(p.x), c0y = __builtin_floorf(p.y), c0z = __builtin_floorf(p.z);
@@ -248,20 +269,22 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   return res;
 }
 
-__device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p) {  // grid_raytracing.cpp:64-89
+template <class CT>
+__device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  // grid_raytracing.cpp:64-89
   const float E = 1e-3f;
   const float xl = (p.x - E >= -1.0f) ? p.x - E : p.x, xr = (p.x + E <= 1.0f) ? p.x + E : p.x;
   const float yl = (p.y - E >= -1.0f) ? p.y - E : p.y, yr = (p.y + E <= 1.0f) ? p.y + E : p.y;
   const float zl = (p.z - E >= -1.0f) ? p.z - E : p.z, zr = (p.z + E <= 1.0f) ? p.z + E : p.z;
-  const float dx = grid_sdf(g, f3{xr, p.y, p.z}, nullptr) - grid_sdf(g, f3{xl, p.y, p.z}, nullptr);
-  const float dy = grid_sdf(g, f3{p.x, yr, p.z}, nullptr) - grid_sdf(g, f3{p.x, yl, p.z}, nullptr);
-  const float dz = grid_sdf(g, f3{p.x, p.y, zr}, nullptr) - grid_sdf(g, f3{p.x, p.y, zl}, nullptr);
+  const float dx = grid_sdf(g, f3{xr, p.y, p.z}, nullptr, cnt) - grid_sdf(g, f3{xl, p.y, p.z}, nullptr, cnt);
+  const float dy = grid_sdf(g, f3{p.x, yr, p.z}, nullptr, cnt) - grid_sdf(g, f3{p.x, yl, p.z}, nullptr, cnt);
+  const float dz = grid_sdf(g, f3{p.x, p.y, zr}, nullptr, cnt) - grid_sdf(g, f3{p.x, p.y, zl}, nullptr, cnt);
   return normalize(f3{dx, dy, dz});
 }
 
 // grid_raytracing.cpp:93-125. Returns hit and leaves the hit point in *hp.
+template <class CT>
 __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
-                                           float &out_t, f3 &hp, uint32_t &cell) {
+                                           float &out_t, f3 &hp, uint32_t &cell, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   float t1, t2;
   bbox_intersection(f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, inv, tNear, tFar, t1, t2);
@@ -271,7 +294,7 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   p = vstd_max(p, f3{-1.0f, -1.0f, -1.0f});
   p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
   while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
-    const float s = grid_sdf(g, p, &cell);
+    const float s = grid_sdf(g, p, &cell, cnt);
     if (s < 1e-3f) {
       out_t = t + s;
       hp = p;
@@ -283,24 +306,28 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   return false;
 }
 
-__device__ __forceinline__ Hit grid_intersect(const GridDev &g, f3 o, f3 d, float tNear, float tFar) {
+template <class CT>
+__device__ __forceinline__ Hit grid_intersect(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
+                                              CT &cnt) {
   Hit h = miss_hit();
   f3 p;
   uint32_t cell;
-  if (grid_march(g, o, d, tNear, tFar, h.t, p, cell)) {
+  if (grid_march(g, o, d, tNear, tFar, h.t, p, cell, cnt)) {
     h.hit = true;
-    h.n = grid_normal(g, p);
+    h.n = grid_normal(g, p, cnt);
     h.prim = (int64_t)cell;
   } else {
     h.t = kInf;
   }
   return h;
 }
-__device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, float tNear, float tFar) {
+template <class CT>
+__device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
+                                              CT &cnt) {
   float t;
   f3 p;
   uint32_t cell;
-  return grid_march(g, o, d, tNear, tFar, t, p, cell);
+  return grid_march(g, o, d, tNear, tFar, t, p, cell, cnt);
 }
 
 // ----------------------------------------------------------------- octree --
@@ -372,10 +399,10 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, f3 bmax, 
 }
 
 // intersectLeaf (octree_raytracing.cpp:122-164) for a leaf that may hit.
-template <bool NEED_NORMAL>
+template <bool NEED_NORMAL, class CT>
 __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax, f3 o,
                                          f3 d, f3 inv, float tNear, float tFar, float &out_t,
-                                         f3 &out_n) {
+                                         f3 &out_n, CT &cnt) {
   float t1, t2;
   bbox_intersection(bmin, bmax, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
@@ -391,9 +418,10 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   while (p.x <= bmax.x && p.y <= bmax.y && p.z <= bmax.z && p.x >= bmin.x && p.y >= bmin.y &&
          p.z >= bmin.z) {
     const float s = oct_sdf(c, bmin, bmax, p);
+    cnt.add(C_OCT_STEP, 1);
     if (s < 1e-4f) {
       out_t = t + s;
-      if (NEED_NORMAL) out_n = oct_normal(c, bmin, bmax, p);
+      if (NEED_NORMAL) { out_n = oct_normal(c, bmin, bmax, p); cnt.add(C_OCT_NORMAL, 1); }
       return true;
     }
     t += s;
@@ -430,17 +458,19 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
   }
 }
 
-template <int BLOCK, bool NEED_NORMAL>
+template <int BLOCK, bool NEED_NORMAL, class CT>
 __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
                                           LdsStack<BLOCK> st, float &out_t, f3 &out_n,
-                                          uint32_t &out_node) {
+                                          uint32_t &out_node, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   const uint32_t root = sc.child[0];
+  cnt.add(C_OCT_NODE, 1);
   if (root == 0 || root == rtl::kOctNeverHits) {
+    cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return false;
     out_node = 0;
     return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, d, inv,
-                                 tNear, tFar, out_t, out_n);
+                                 tNear, tFar, out_t, out_n, cnt);
   }
   // top frame: node whose children are being visited, its coords and list
   uint32_t fnode = 0, flist, fcnt;
@@ -468,11 +498,13 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
     const uint32_t cn = sc.child[fnode] + j;
     const uint32_t cx = (ix << 1) | (j >> 2), cy = (iy << 1) | ((j >> 1) & 1u), cz = (iz << 1) | (j & 1u);
     const uint32_t cw = sc.child[cn];
-    if (cw == rtl::kOctNeverHits) continue;
+    cnt.add(C_OCT_NODE, 1);
+    if (cw == rtl::kOctNeverHits) { cnt.add(C_OCT_LEAF, 1); continue; }
     f3 bmin, bmax;
     oct_box(cx, cy, cz, depth + 1, bmin, bmax);
     if (cw == 0) {
-      if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, o, d, inv, tNear, tFar, out_t, out_n)) {
+      cnt.add(C_OCT_LEAF, 1);
+      if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, o, d, inv, tNear, tFar, out_t, out_n, cnt)) {
         out_node = cn;
         return true;
       }
@@ -489,12 +521,12 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
   }
 }
 
-template <int BLOCK>
+template <int BLOCK, class CT>
 __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK> st) {
+                                             LdsStack<BLOCK> st, CT &cnt) {
   Hit h = miss_hit();
   uint32_t node;
-  if (oct_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, h.t, h.n, node)) {
+  if (oct_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, h.t, h.n, node, cnt)) {
     h.hit = true;
     h.prim = (int64_t)node;
   } else {
@@ -502,13 +534,13 @@ __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float
   }
   return h;
 }
-template <int BLOCK>
+template <int BLOCK, class CT>
 __device__ __forceinline__ bool oct_occluded(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK> st) {
+                                             LdsStack<BLOCK> st, CT &cnt) {
   float t;
   f3 n;
   uint32_t node;
-  return oct_trace<BLOCK, false>(sc, o, d, tNear, tFar, st, t, n, node);
+  return oct_trace<BLOCK, false>(sc, o, d, tNear, tFar, st, t, n, node, cnt);
 }
 
 // ------------------------------------------------------------------ plane --

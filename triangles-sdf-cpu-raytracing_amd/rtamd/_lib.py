@@ -77,6 +77,8 @@ _SIGS = {
     "rt_tile_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_float,
                                     C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_count_work": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                C.c_uint32, C.c_void_p, C.c_void_p]),
     "rt_bench_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
 }

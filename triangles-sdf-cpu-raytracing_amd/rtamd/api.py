@@ -225,6 +225,30 @@ class IScene:
                                     RT_FLAG_CLEAR if clear else 0, C.byref(mean), C.byref(total)))
         return mean.value, total.value
 
+    COUNTER_NAMES = ("bvh_inner", "bvh_leaf", "bvh_tri", "grid_sdf", "oct_node", "oct_leaf",
+                     "oct_step", "oct_normal", "rays")
+
+    def count_work(self, params_list, W: int, H: int, clear: bool = True,
+                   tile: Tile | None = None) -> dict:
+        """Reference-traversal work counters over the given frames (rt_count_work)."""
+        arr = (RenderParams * len(params_list))(*params_list)
+        out = np.zeros(9, np.int64)
+        check(lib().rt_count_work(self._handle(), arr, len(params_list), W, H,
+                                  RT_FLAG_CLEAR if clear else 0,
+                                  C.byref(tile) if tile is not None else None, _p(out)))
+        return dict(zip(self.COUNTER_NAMES, out.tolist()))
+
+    @staticmethod
+    def algorithmic_bytes(c: dict, pixels: int) -> int:
+        """Bytes the reference's data layout touches for this work:
+        BVH 200 B / inner-node visit (Box8 + realCount + offset), 8 B / leaf visit,
+        60 B / triangle test (3 indices + 3 float4 vertices); grid 32 B / sdf
+        evaluation (8 taps); octree 4 B / node visit, 32 B / leaf visit, 32 B /
+        march step, 32 B / normal; + 8 B / pixel of framebuffer (colour + t)."""
+        return int(200 * c["bvh_inner"] + 8 * c["bvh_leaf"] + 60 * c["bvh_tri"] + 32 * c["grid_sdf"]
+                   + 4 * c["oct_node"] + 32 * c["oct_leaf"] + 32 * c["oct_step"]
+                   + 32 * c["oct_normal"] + 8 * pixels)
+
     def device_bytes(self) -> int:
         return int(lib().rt_scene_device_bytes(self._handle()))
 
