@@ -161,3 +161,20 @@ def test_no_fallback_library_loaded(gpu):
     import rtamd
     assert rtamd.lib()._name.endswith("librtamd.so")
     assert rtamd.device_count() >= 1
+
+
+def test_golden_fixture_frames(gpu):
+    """GPU frames equal the committed oracle fixtures (tests/golden/frames.npz)."""
+    import importlib.util
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(here, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    data = np.load(os.path.join(here, "frames.npz"))
+    index = json.load(open(os.path.join(here, "frames.json")))
+    for case, ent in zip(mg.CASES, index):
+        name, W, H, mode, pos = case
+        c, t = S.gpu_frame(name, W, H, mode, pos)
+        assert_same((data[ent["color"]], data[ent["t"]]), (c, t), ent["case"])
