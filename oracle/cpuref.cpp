@@ -1126,6 +1126,51 @@ double cpuref_render(void *h, const RefParams *P, uint32_t *color, float *tbuf, 
   return std::chrono::duration<double, std::milli>(e - b).count();
 }
 
+// Per-pixel work of the primary ray (oracle bookkeeping for performance
+// analysis): cost[y*W+x] = bvh_inner + bvh_leaf + bvh_tri + grid_sdf +
+// oct_node + oct_leaf + oct_step for that pixel's primary intersection.
+void cpuref_pixel_cost(void *h, const RefParams *P, int W, int H, int32_t *cost) {
+  RefScene *s = (RefScene *)h;
+  const IScene *base = s->base();
+  float4x4 viewInv, projInv;
+  std::memcpy(viewInv.m, P->view_inv, 64);
+  std::memcpy(projInv.m, P->proj_inv, 64);
+  float3 rayPos(P->camera_pos[0], P->camera_pos[1], P->camera_pos[2]);
+#pragma omp parallel for schedule(dynamic)
+  for (int yo = 0; yo < H; ++yo) {
+    int y = H - yo - 1;
+    for (int x = 0; x < W; ++x) {
+      float4 dir4 = EyeRayDir4f((float)x + 0.5f, (float)y + 0.5f, (float)W, (float)H, projInv);
+      dir4.w = 0.0f;
+      dir4 = mul(viewInv, dir4);
+      Counters before = tl_cnt;
+      base->intersect(rayPos, to_float3(dir4), 0.01f, 100.0f);
+      const Counters &a = tl_cnt;
+      cost[(size_t)yo * W + x] = (int32_t)((a.bvh_inner - before.bvh_inner) + (a.bvh_leaf - before.bvh_leaf) +
+                                           (a.bvh_tri - before.bvh_tri) + (a.grid_sdf - before.grid_sdf) +
+                                           (a.oct_node - before.oct_node) + (a.oct_leaf - before.oct_leaf) +
+                                           (a.oct_step - before.oct_step));
+    }
+  }
+}
+
+// Primary rays of a frame (origin shared): dirs[(y*W+x)*3..] in image layout.
+void cpuref_primary_rays(const RefParams *P, int W, int H, float *dirs) {
+  float4x4 viewInv, projInv;
+  std::memcpy(viewInv.m, P->view_inv, 64);
+  std::memcpy(projInv.m, P->proj_inv, 64);
+  for (int yo = 0; yo < H; ++yo) {
+    int y = H - yo - 1;
+    for (int x = 0; x < W; ++x) {
+      float4 d4 = EyeRayDir4f((float)x + 0.5f, (float)y + 0.5f, (float)W, (float)H, projInv);
+      d4.w = 0.0f;
+      d4 = mul(viewInv, d4);
+      size_t i = ((size_t)yo * W + x) * 3;
+      dirs[i] = d4.x; dirs[i + 1] = d4.y; dirs[i + 2] = d4.z;
+    }
+  }
+}
+
 // Ray-level entry: intersect arbitrary rays against the scene (union with plane
 // if enabled). hit[i] in {0,1}; t, normal as in HitInfo; prim id as documented.
 void cpuref_intersect_rays(void *h, const float *o, const float *d, int64_t n, float tNear, float tFar,

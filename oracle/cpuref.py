@@ -55,6 +55,8 @@ def lib():
         L.cpuref_render.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
         L.cpuref_intersect_rays.argtypes = [vp, vp, vp, i64, f32, f32, vp, vp, vp, vp]
         L.cpuref_counters.argtypes = [C.c_int, vp]
+        L.cpuref_pixel_cost.argtypes = [vp, vp, C.c_int, C.c_int, vp]
+        L.cpuref_primary_rays.argtypes = [vp, C.c_int, C.c_int, vp]
         L.cpuref_fnv1a64.restype = C.c_uint64
         L.cpuref_fnv1a64.argtypes = [vp, i64]
         _lib = L
@@ -167,6 +169,12 @@ class RefScene:
                                  threads, None)
         return color, t, pr, ms
 
+    def pixel_cost(self, params: RefParams, W: int, H: int):
+        """Per-pixel primary-ray work (node visits + leaf visits + tests/steps)."""
+        cost = np.zeros((H, W), np.int32)
+        lib().cpuref_pixel_cost(self.h, C.byref(params), W, H, _p(cost))
+        return cost
+
     def intersect_rays(self, o, d, tnear=0.01, tfar=100.0):
         o = np.ascontiguousarray(o, np.float32)
         d = np.ascontiguousarray(d, np.float32)
@@ -183,6 +191,13 @@ class RefScene:
         if getattr(self, "h", None) and _lib is not None:
             _lib.cpuref_scene_free(self.h)
             self.h = None
+
+
+def primary_rays(params: RefParams, W: int, H: int) -> np.ndarray:
+    """World-space primary ray directions [H, W, 3] (Renderer::draw ray generation)."""
+    d = np.zeros((H, W, 3), np.float32)
+    lib().cpuref_primary_rays(C.byref(params), W, H, _p(d))
+    return d
 
 
 def fnv1a64_words(color: np.ndarray) -> str:

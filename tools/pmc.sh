@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes (one counter group per rocprofv3 run; no trace domains with --pmc).
+# usage: tools/pmc.sh <outdir> <workload> [frames]
+set -e
+OUT=${1:-gpurun_out/pmc}; WL=${2:-stanford-bunny.obj}; N=${3:-16}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+run() { name=$1; shift
+  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o p -- \
+    python3 tools/prof_frames.py --workload $WL --frames $N > $OUT/$name.log 2>&1 || { echo "pass $name failed"; tail -5 $OUT/$name.log; exit 1; }
+}
+run fetch FETCH_SIZE
+run write WRITE_SIZE
+run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
+run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum
+run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum
+echo done

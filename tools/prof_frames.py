@@ -1,0 +1,28 @@
+"""Render N orbit frames of one workload back to back (profiling driver)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd"))
+import torch  # noqa: F401,E402  (one HIP runtime)
+import rtamd  # noqa: E402
+from rtamd import workloads as WL  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="stanford-bunny.obj")
+ap.add_argument("--frames", type=int, default=16)
+ap.add_argument("--W", type=int, default=1920)
+ap.add_argument("--H", type=int, default=1080)
+ap.add_argument("--mode", default="primary")
+a = ap.parse_args()
+kind, payload, off = WL.load_input(a.workload)
+s = WL.make_scene(kind, payload)
+if a.mode == "primary":
+    s.set_plane(None)
+    P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Normal) for p in WL.orbit_positions(64)]
+else:
+    s.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off))
+    P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Lambert) for p in WL.orbit_positions(64)]
+mean, total = s.bench_frames([P[k % 64] for k in range(a.frames)], a.W, a.H)
+print(f"{a.workload} {a.W}x{a.H} {a.mode}: {mean:.4f} ms/frame", flush=True)

@@ -48,42 +48,47 @@ struct FrameArgs {
 };
 
 // ---------------------------------------------------------- scene adapters --
+// kFields = LDS words per traversal frame (mesh: node, list|count, best t;
+// octree: node, list|count; grid: none).
 struct MeshS {
+  static constexpr int kFields = 3;
   MeshDev d;
   template <int B, class CT>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
-                                           CT &cnt) const {
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields> st, CT &cnt) const {
     return mesh_intersect<B>(d, o, dir, tn, tf, st, cnt);
   }
   template <int B, class CT>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
-                                           CT &cnt) const {
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields> st, CT &cnt) const {
     return mesh_occluded<B>(d, o, dir, tn, tf, st, cnt);
   }
 };
 struct GridS {
+  static constexpr int kFields = 1;
   GridDev d;
   template <int B, class CT>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B>,
-                                           CT &cnt) const {
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields>, CT &cnt) const {
     return grid_intersect(d, o, dir, tn, tf, cnt);
   }
   template <int B, class CT>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B>,
-                                           CT &cnt) const {
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields>, CT &cnt) const {
     return grid_occluded(d, o, dir, tn, tf, cnt);
   }
 };
 struct OctS {
+  static constexpr int kFields = 2;
   OctDev d;
   template <int B, class CT>
-  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
-                                           CT &cnt) const {
+  __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields> st, CT &cnt) const {
     return oct_intersect<B>(d, o, dir, tn, tf, st, cnt);
   }
   template <int B, class CT>
-  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf, LdsStack<B> st,
-                                           CT &cnt) const {
+  __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
+                                           LdsStack<B, kFields> st, CT &cnt) const {
     return oct_occluded<B>(d, o, dir, tn, tf, st, cnt);
   }
 };
@@ -97,7 +102,7 @@ struct SurfHit {
 };
 template <class S, int B, class CT>
 __device__ __forceinline__ SurfHit union_intersect(const S &sc, const PlaneDev &pl, f3 o, f3 d,
-                                                   float tn, float tf, LdsStack<B> st, CT &cnt) {
+                                                   float tn, float tf, LdsStack<B, S::kFields> st, CT &cnt) {
   cnt.add(C_RAYS, 1);
   SurfHit r{sc.template intersect<B>(o, d, tn, tf, st, cnt), 1.0f, 0.0f};
   if (pl.on) {
@@ -120,7 +125,7 @@ __device__ __forceinline__ SurfHit union_intersect(const S &sc, const PlaneDev &
 // Shadow query: HitInfo::hitten of the union is the OR of both hitten flags.
 template <class S, int B, class CT>
 __device__ __forceinline__ bool union_occluded(const S &sc, const PlaneDev &pl, f3 o, f3 d, float tn,
-                                               float tf, LdsStack<B> st, CT &cnt) {
+                                               float tf, LdsStack<B, S::kFields> st, CT &cnt) {
   cnt.add(C_RAYS, 1);
   if (sc.template occluded<B>(o, d, tn, tf, st, cnt)) return true;
   if (pl.on) {
@@ -135,7 +140,7 @@ __device__ __forceinline__ bool union_occluded(const S &sc, const PlaneDev &pl, 
 template <class S, int B, class CT>
 __device__ __forceinline__ f4 lambert_color(const S &sc, const PlaneDev &pl,
                                             const rt_render_params &P, f3 o, f3 d,
-                                            const SurfHit &sh, f3 n, LdsStack<B> st, CT &cnt) {
+                                            const SurfHit &sh, f3 n, LdsStack<B, S::kFields> st, CT &cnt) {
   bool visible = true;
   const f3 point = o + sh.h.t * d;
   const f3 L{P.light_pos[0], P.light_pos[1], P.light_pos[2]};
@@ -154,7 +159,7 @@ __device__ __forceinline__ f4 lambert_color(const S &sc, const PlaneDev &pl,
 template <class S, int B, class CT>
 __device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const rt_render_params &P,
                                         f3 o, f3 d, float tFarEff, bool allow_refl, bool &hit,
-                                        float &t_out, LdsStack<B> st, int64_t *prim, CT &cnt) {
+                                        float &t_out, LdsStack<B, S::kFields> st, int64_t *prim, CT &cnt) {
   const SurfHit sh = union_intersect<S, B>(sc, pl, o, d, 0.01f, tFarEff, st, cnt);
   if (prim) *prim = sh.h.hit ? sh.h.prim : -1;
   if (!sh.h.hit) {
@@ -192,6 +197,25 @@ __device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const r
   return c;
 }
 
+// Framebuffer stores. The frame (8 B/pixel, 16.6 MB at 1080p) is written once
+// and never re-read by the kernel; plain stores keep every written line in the
+// XCD's 4 MiB L2 and push scene data out. Agent-scope relaxed atomic stores
+// lower to `global_store ... sc1`, which the MI355X L2 drops after writing.
+__device__ __forceinline__ void fb_store(uint32_t *p, uint32_t v) {
+#ifdef RT_PLAIN_FB_STORES
+  *p = v;
+#else
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+__device__ __forceinline__ void fb_store(float *p, float v) {
+#ifdef RT_PLAIN_FB_STORES
+  *p = v;
+#else
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
 __device__ __forceinline__ int image_row(int yl, const FrameArgs &fa) {
   if (fa.nranks <= 1) return yl;
   const int k = yl / fa.band_rows, r = yl - k * fa.band_rows;
@@ -201,12 +225,17 @@ __device__ __forceinline__ int image_row(int yl, const FrameArgs &fa) {
 // Renderer::draw (raytracing.cpp:67-102). GENERAL=false is the primary-ray
 // path (Normal shading, no plane, no secondary rays) used by the headline
 // benchmark; GENERAL=true runs intersectionColor in full.
-// COUNT=true is a diagnostic variant that also accumulates the work counters
-// (algorithmic-bytes model) into counters[C_NUM]; the timed kernels use COUNT=false.
-template <bool COUNT>
+// DIAG selects diagnostic variants of the same kernel (the timed kernels use 0):
+//   1: accumulate the work counters (algorithmic-bytes model) into diag[C_NUM];
+//   2: per-wave timestamps: diag[4*w .. 4*w+3] = start, end (s_memrealtime,
+//      100 MHz), (sum << 32 | max) over lanes of work units, XCC_ID register;
+//      w = linear block * 4 + wave.
+template <int DIAG>
 struct CntSel { using T = NoCnt; };
 template <>
-struct CntSel<true> { using T = LaneCnt; };
+struct CntSel<1> { using T = LaneCnt; };
+template <>
+struct CntSel<2> { using T = LaneCnt; };
 
 __device__ __forceinline__ void flush_counts(NoCnt &, unsigned long long *) {}
 __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out) {
@@ -219,18 +248,27 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
   }
 }
 
-template <class S, int MAXD, bool GENERAL, bool COUNT>
+// Block -> tile map: plain 2-D dispatch (tiles dealt round-robin over the 8
+// XCDs in blockIdx order). Measured and rejected: one contiguous band of tiles
+// per XCD (GEMM-style XCD swizzle: the XCD owning the model's band becomes the
+// tail; bunny 0.356 -> 0.378 ms, octree 4K default 1.72 -> 2.30 ms) and a
+// centre-out order that dispatches the model tiles first (octree 4K primary
+// 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
+
+template <class S, int SLOTS, bool GENERAL, int DIAG>
 __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
-  __shared__ uint32_t stk[MAXD * 3 * kBlock];
-  typename CntSel<COUNT>::T cnt{};
+  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  typename CntSel<DIAG>::T cnt{};
+  unsigned long long t_start = 0;
+  if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
   const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
   const bool active = xo < fa.W && yl < fa.rows_local;
-  if (!COUNT && !active) return;
+  if (DIAG == 0 && !active) return;
   if (active) {  // (the counting variant keeps every lane for its wave reduction)
-    LdsStack<kBlock> st{stk + threadIdx.x};
+    LdsStack<kBlock, S::kFields> st{stk + threadIdx.x};
     const int yo = image_row(yl, fa);
     const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
     const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
@@ -256,26 +294,137 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
     // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
     const bool store = hit && !__builtin_isinf(t);
     if (clear) {
-      fa.color[idx] = store ? pack_rgba(c) : 0u;
-      fa.t[idx] = store ? t : kInf;
+      fb_store(fa.color + idx, store ? pack_rgba(c) : 0u);
+      fb_store(fa.t + idx, store ? t : kInf);
     } else if (store) {
-      fa.color[idx] = pack_rgba(c);
-      fa.t[idx] = t;
+      fb_store(fa.color + idx, pack_rgba(c));
+      fb_store(fa.t + idx, t);
     }
   }
-  flush_counts(cnt, counters);
+  if constexpr (DIAG == 1) flush_counts(cnt, counters);
+  if constexpr (DIAG == 2) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    // this lane's sequential work units (node/leaf visits, tests, steps, sdf evals)
+    uint32_t units = 0;
+#pragma unroll
+    for (int i = 0; i < C_RAYS; ++i) units += cnt.v[i];
+    uint32_t mx = units, sm = units;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t om = __shfl_xor(mx, off, 64), os = __shfl_xor(sm, off, 64);
+      mx = mx > om ? mx : om;
+      sm += os;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+      counters[4 * w] = t_start;
+      counters[4 * w + 1] = t_end;
+      counters[4 * w + 2] = ((unsigned long long)sm << 32) | mx;
+      counters[4 * w + 3] = __builtin_amdgcn_s_getreg(0x1814);  // HW_REG_XCC_ID, 4 bits
+    }
+  }
+}
+
+// ---- two-kernel (wavefront) primary path for meshes -------------------------
+// Renderer::draw with Normal shading and no plane, split at the root: K1 does
+// ray generation and the root stage for every pixel, resolves the rays that
+// enter no root child (86% at 1080p on the bunny), and compacts the others into
+// a queue (wave ballot + prefix count, one atomic per wave); K2 traces only the
+// queued rays. Heavy rays then all start together at the top of K2 instead of
+// being spread over a long dispatch that is mostly trivial waves.
+struct alignas(16) QEntry {
+  uint32_t pix;      // yl * W + xo (packed-row index)
+  float dx, dy, dz;  // world ray direction
+  uint32_t list;     // root frame: remaining children | count << 24
+  float tfirst;      // entry t of the first child
+  uint32_t cwfirst;  // child word of the first child
+  float tfar;        // std::min(100, tPrev)
+};
+
+__device__ __forceinline__ f4 normal_color(f3 n, f3 d) {
+  if (dot(n, d) > 0) n = n * -1.0f;
+  return f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
+}
+
+__global__ __launch_bounds__(kBlock) void mesh_primary_k1(MeshDev sc, FrameArgs fa, QEntry *q,
+                                                          uint32_t *qcount) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
+  const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  const bool active = xo < fa.W && yl < fa.rows_local;
+  bool survive = false;
+  QEntry e;
+  if (active) {
+    const int yo = image_row(yl, fa);
+    const int y = fa.H - yo - 1;
+    const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
+    const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+    const size_t idx = (size_t)yl * fa.W + xo;
+    const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
+    const float tPrev = clear ? kInf : fa.t[idx];
+    const float tFarEff = std_min(100.0f, tPrev);
+    const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    uint32_t l = 0, c = 0, cwf = 0;
+    float tf = 0.0f;
+    NoCnt nc;
+    survive = mesh_root(sc, o, inv, 0.01f, tFarEff, l, c, tf, cwf, nc);
+    if (survive) {
+      e = QEntry{(uint32_t)idx, d.x, d.y, d.z, l | (c << 24), tf, cwf, tFarEff};
+    } else if (clear) {
+      fa.color[idx] = 0u;
+      fa.t[idx] = kInf;
+    }
+  }
+  const unsigned long long m = __ballot(survive);
+  if (m == 0) return;
+  const uint32_t n = (uint32_t)__popcll(m);
+  const int leader = __builtin_ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(qcount, n);
+  base = (uint32_t)__shfl((int)base, leader, 64);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (survive) q[base + rank] = e;
+}
+
+template <int SLOTS>
+__global__ __launch_bounds__(kBlock) void mesh_primary_k2(MeshDev sc, FrameArgs fa, const QEntry *q,
+                                                          const uint32_t *qcount) {
+  __shared__ uint32_t stk[SLOTS * 3 * kBlock];
+  LdsStack<kBlock> st{stk + threadIdx.x};
+  const uint32_t n = *qcount;
+  const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
+  NoCnt nc;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const QEntry e = q[i];
+    const f3 d{e.dx, e.dy, e.dz};
+    const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    float t;
+    uint32_t k;
+    const bool hit = mesh_continue<kBlock, false>(sc, o, d, inv, 0.01f, e.tfar, st, rtl::kInvalidChild,
+                                                  e.list & 0xFFFFFFu, e.list >> 24, e.tfirst, e.cwfirst,
+                                                  true, 1, t, k, nc);
+    const bool store = hit && !__builtin_isinf(t);
+    const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
+    if (store) {
+      fa.color[e.pix] = pack_rgba(normal_color(tri_normal(sc.tris, k), d));
+      fa.t[e.pix] = t;
+    } else if (clear) {
+      fa.color[e.pix] = 0u;
+      fa.t[e.pix] = kInf;
+    }
+  }
 }
 
 // IScene::intersect over a batch of rays (union with the plane if enabled).
-template <class S, int MAXD>
+template <class S, int SLOTS>
 __global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const float *o3,
                                                        const float *d3, int64_t n, float tn,
                                                        float tf, int32_t *hit, float *t,
                                                        float *nrm, int64_t *prim) {
-  __shared__ uint32_t stk[MAXD * 3 * kBlock];
+  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  LdsStack<kBlock> st{stk + threadIdx.x};
+  LdsStack<kBlock, S::kFields> st{stk + threadIdx.x};
   const f3 o{o3[3 * i], o3[3 * i + 1], o3[3 * i + 2]};
   const f3 d{d3[3 * i], d3[3 * i + 1], d3[3 * i + 2]};
   NoCnt cnt;
@@ -310,6 +459,7 @@ struct rt_scene {
   rtl::GNode *d_nodes = nullptr;
   rtl::GTri *d_tris = nullptr;
   uint32_t root = rtl::kInvalidChild;
+  float root_box[6] = {0, 0, 0, 0, 0, 0};
   int64_t host_nodes = 0, host_inner = 0;
   int32_t bvh_depth = 0;
   // grid
@@ -325,16 +475,33 @@ struct rt_scene {
   uint32_t *d_color = nullptr;
   float *d_t = nullptr;
   size_t fb_cap = 0;
+  // wavefront queue (mesh primary path), sized to the largest frame rendered
+  QEntry *d_queue = nullptr;
+  uint32_t *d_qcount = nullptr;
+  size_t q_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // A/B switch: two-kernel wavefront primary path. Off by default: measured
+  // slower (bunny 1080p 0.417 vs 0.330 ms): concentrating the heavy rays in
+  // K2 raises their memory latency more than it saves in scheduling.
+  bool use_wavefront = false;
 };
 
 namespace {
 
+MeshDev mesh_dev(const rt_scene *s) {
+  MeshDev m{s->d_nodes, s->d_tris, s->root, {}};
+  for (int k = 0; k < 6; ++k) m.rbox[k] = s->root_box[k];
+  return m;
+}
+
+// LDS frame slots per lane for a tree with `depth` inner levels: the top frame
+// lives in registers, so depth-1 slots. Sized to the tree (not a worst case)
+// so the stack does not cap occupancy: 4 slots x 12 B x 256 lanes = 12 KiB.
 int pick_maxd(int depth, int32_t &maxd) {
-  // LDS frames per lane: MAXD*12 B; 32 levels = 96 KiB per 256-lane workgroup.
-  const int options[] = {8, 16, 32};
+  const int need = depth > 1 ? depth - 1 : 1;
+  const int options[] = {4, 7, 15, 31};
   for (int m : options)
-    if (depth <= m) { maxd = m; return RT_OK; }
+    if (need <= m) { maxd = m; return RT_OK; }
   return set_err(RT_E_INVALID, "tree deeper than 32 levels");
 }
 
@@ -359,40 +526,82 @@ int ensure_fb(rt_scene *s, size_t px) {
 
 template <class S, int MAXD>
 void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool general,
-                     hipStream_t stream, unsigned long long *counters) {
+                     hipStream_t stream, unsigned long long *counters, int diag) {
   const dim3 grid((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
-  if (counters) {
+  if (diag == 1) {
     if (general)
-      render_kernel<S, MAXD, true, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+      render_kernel<S, MAXD, true, 1><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
     else
-      render_kernel<S, MAXD, false, true><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+      render_kernel<S, MAXD, false, 1><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+  } else if (diag == 2) {
+    if (general)
+      render_kernel<S, MAXD, true, 2><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
+    else
+      render_kernel<S, MAXD, false, 2><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
   } else {
     if (general)
-      render_kernel<S, MAXD, true, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+      render_kernel<S, MAXD, true, 0><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
     else
-      render_kernel<S, MAXD, false, false><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+      render_kernel<S, MAXD, false, 0><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
   }
 }
 
+int ensure_queue(rt_scene *s, size_t n) {
+  if (n <= s->q_cap) return RT_OK;
+  if (s->d_queue) (void)hipFree(s->d_queue);
+  s->d_queue = nullptr;
+  s->q_cap = 0;
+  HIP_TRY(hipMalloc(&s->d_queue, n * sizeof(QEntry)));
+  if (!s->d_qcount) HIP_TRY(hipMalloc(&s->d_qcount, 64));
+  s->q_cap = n;
+  return RT_OK;
+}
+
+int launch_mesh_primary(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
+  const size_t px = (size_t)fa.W * fa.rows_local;
+  int rc = ensure_queue(s, px);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(s->d_qcount, 0, 4, stream));
+  const MeshDev md = mesh_dev(s);
+  const dim3 g1((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
+  mesh_primary_k1<<<g1, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount);
+  // K2: enough workgroups to hold every queued ray in one pass when they fit
+  // the machine, grid-stride beyond that.
+  const unsigned g2 = (unsigned)std::min<size_t>((px + kBlock - 1) / kBlock, 4096);
+  switch (s->maxd) {
+    case 4: mesh_primary_k2<4><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
+    case 7: mesh_primary_k2<7><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
+    case 15: mesh_primary_k2<15><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
+    default: mesh_primary_k2<31><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
 int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream,
-                  unsigned long long *counters = nullptr) {
+                  unsigned long long *counters = nullptr, int diag = 0) {
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
+  if (s->kind == RT_SCENE_MESH && !general && diag == 0 && s->root != rtl::kInvalidChild &&
+      !(s->root & rtl::kLeafBit) && s->use_wavefront)
+    return launch_mesh_primary(s, fa, stream);
   if (s->kind == RT_SCENE_MESH) {
-    MeshS sc{MeshDev{s->d_nodes, s->d_tris, s->root}};
+    MeshS sc{mesh_dev(s)};
     switch (s->maxd) {
-      case 8: launch_render_t<MeshS, 8>(sc, s->plane, fa, general, stream, counters); break;
-      case 16: launch_render_t<MeshS, 16>(sc, s->plane, fa, general, stream, counters); break;
-      default: launch_render_t<MeshS, 32>(sc, s->plane, fa, general, stream, counters); break;
+      case 4: launch_render_t<MeshS, 4>(sc, s->plane, fa, general, stream, counters, diag); break;
+      case 7: launch_render_t<MeshS, 7>(sc, s->plane, fa, general, stream, counters, diag); break;
+      case 15: launch_render_t<MeshS, 15>(sc, s->plane, fa, general, stream, counters, diag); break;
+      default: launch_render_t<MeshS, 31>(sc, s->plane, fa, general, stream, counters, diag); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
     GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
-    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream, counters);
+    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream, counters, diag);
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
-      case 8: launch_render_t<OctS, 8>(sc, s->plane, fa, general, stream, counters); break;
-      case 16: launch_render_t<OctS, 16>(sc, s->plane, fa, general, stream, counters); break;
-      default: launch_render_t<OctS, 32>(sc, s->plane, fa, general, stream, counters); break;
+      case 4: launch_render_t<OctS, 4>(sc, s->plane, fa, general, stream, counters, diag); break;
+      case 7: launch_render_t<OctS, 7>(sc, s->plane, fa, general, stream, counters, diag); break;
+      case 15: launch_render_t<OctS, 15>(sc, s->plane, fa, general, stream, counters, diag); break;
+      default: launch_render_t<OctS, 31>(sc, s->plane, fa, general, stream, counters, diag); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
@@ -450,6 +659,16 @@ int new_scene(rt_scene **out) {
   s->plane.on = 0;
   s->plane.n = f3{0.0f, 1.0f, 0.0f};
   *out = s;
+  return RT_OK;
+}
+
+// upload + `pad` zeroed trailing elements (kernels may read past the end).
+template <class T>
+int upload_padded(T **dst, const T *src, size_t n, size_t pad, int64_t &bytes) {
+  HIP_TRY(hipMalloc(dst, (n + pad) * sizeof(T)));
+  HIP_TRY(hipMemset(*dst, 0, (n + pad) * sizeof(T)));
+  if (n) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  bytes += (int64_t)((n + pad) * sizeof(T));
   return RT_OK;
 }
 
@@ -563,11 +782,12 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
   s->kind = RT_SCENE_MESH;
   s->maxd = maxd;
   s->root = b.root_word;
+  std::memcpy(s->root_box, b.root_box, sizeof(s->root_box));
   s->host_nodes = b.host_nodes;
   s->host_inner = b.host_inner;
   s->bvh_depth = b.max_depth;
   if ((rc = upload(&s->d_nodes, b.nodes.data(), b.nodes.size(), s->dev_bytes)) ||
-      (rc = upload(&s->d_tris, b.tris.data(), b.tris.size(), s->dev_bytes))) {
+      (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes))) {
     rt_scene_destroy(s);
     return rc;
   }
@@ -658,7 +878,8 @@ int rt_scene_destroy(rt_scene *s) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(s->device);
-  void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t};
+  void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t,
+                  s->d_queue, s->d_qcount};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -748,11 +969,12 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
         (e = hipMemcpy(dD, d, n * 12, hipMemcpyHostToDevice)))
       break;
     if (s->kind == RT_SCENE_MESH) {
-      MeshS sc{MeshDev{s->d_nodes, s->d_tris, s->root}};
+      MeshS sc{mesh_dev(s)};
       switch (s->maxd) {
-        case 8: launch_rays_t<MeshS, 8>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        case 16: launch_rays_t<MeshS, 16>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        default: launch_rays_t<MeshS, 32>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 4: launch_rays_t<MeshS, 4>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 7: launch_rays_t<MeshS, 7>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 15: launch_rays_t<MeshS, 15>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        default: launch_rays_t<MeshS, 31>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     } else if (s->kind == RT_SCENE_GRID) {
       GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
@@ -760,9 +982,10 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
     } else {
       OctS sc{OctDev{s->d_child, s->d_ovals}};
       switch (s->maxd) {
-        case 8: launch_rays_t<OctS, 8>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        case 16: launch_rays_t<OctS, 16>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        default: launch_rays_t<OctS, 32>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 4: launch_rays_t<OctS, 4>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 7: launch_rays_t<OctS, 7>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 15: launch_rays_t<OctS, 15>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        default: launch_rays_t<OctS, 31>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     }
     if ((e = hipGetLastError())) break;
@@ -792,7 +1015,7 @@ int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, i
     FrameArgs fa;
     if (!(rc = check_params(params + f, W, H)) &&
         !(rc = fill_frame(fa, params + f, s->d_color, s->d_t, W, H, flags, tile)))
-      rc = launch_render(s, fa, 0, d);
+      rc = launch_render(s, fa, 0, d, 1);
   }
   unsigned long long h[C_NUM] = {};
   if (e == hipSuccess && rc == RT_OK) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
@@ -800,6 +1023,38 @@ int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, i
   if (rc) return rc;
   if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rt_count_work: ") + hipGetErrorString(e));
   for (int i = 0; i < C_NUM; ++i) counters[i] = (int64_t)h[i];
+  return RT_OK;
+}
+
+// Diagnostic (not part of include/rtamd.h): per-wave timestamps of one frame.
+// out: 4 x u64 per wave (see DIAG == 2); *nwaves in/out: capacity / written.
+int rtx_wave_stamps(rt_scene *s, const rt_render_params *params, int32_t W, int32_t H, uint32_t flags,
+                    uint64_t *out, int64_t *nwaves) {
+  if (!s || !params || !out || !nwaves) return set_err(RT_E_INVALID, "bad arguments");
+  int rc = check_params(params, W, H);
+  if (rc) return rc;
+  const int64_t nb = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  const int64_t nw = nb * (kBlock / 64);
+  if (*nwaves < nw) { *nwaves = nw; return set_err(RT_E_INVALID, "buffer too small"); }
+  const size_t px = (size_t)W * H;
+  if ((rc = ensure_fb(s, px))) return rc;
+  unsigned long long *d = nullptr;
+  HIP_TRY(hipMalloc(&d, nw * 4 * sizeof(unsigned long long)));
+  FrameArgs fa;
+  if (!(rc = fill_frame(fa, params, s->d_color, s->d_t, W, H, flags, nullptr)))
+    rc = launch_render(s, fa, 0, d, 2);
+  hipError_t e = rc ? hipSuccess : hipMemcpy(out, d, nw * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (rc) return rc;
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
+  *nwaves = nw;
+  return RT_OK;
+}
+
+// Diagnostic: two-kernel wavefront path for mesh primary rays (A/B).
+int rtx_set_wavefront(rt_scene *s, int on) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  s->use_wavefront = on != 0;
   return RT_OK;
 }
 

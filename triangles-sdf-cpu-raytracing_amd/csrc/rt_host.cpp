@@ -503,6 +503,12 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     }
   }
   out.root_word = 0;
+  {
+    const HNode &r = H[0];
+    Box u = empty_box();
+    for (uint32_t c = 0; c < r.nchild; ++c) grow(u, r.box[c]);
+    for (int k = 0; k < 3; ++k) { out.root_box[k] = u.mn[k]; out.root_box[3 + k] = u.mx[k]; }
+  }
   return true;
 }
 

@@ -25,6 +25,7 @@ struct BVHGpu {
   std::vector<rtl::GNode> nodes;   // inner nodes, BFS order, root = 0
   std::vector<rtl::GTri> tris;     // leaf triangles, leaves in BFS order of their parents
   uint32_t root_word = rtl::kInvalidChild;
+  float root_box[6] = {0, 0, 0, 0, 0, 0};  // union of the root's child boxes (inner root)
   int32_t max_depth = 0;           // inner nodes on the deepest root->leaf path
   int64_t host_nodes = 0, host_inner = 0;
   // canonical pre-order export (52 x u32 per node), for parity with the oracle

@@ -51,26 +51,28 @@ struct MeshDev {
   const rtl::GNode *__restrict__ nodes;
   const rtl::GTri *__restrict__ tris;
   uint32_t root;
+  // union of the root's child boxes (exact min/max of their floats): a ray that
+  // misses it under the slab formula misses every child (the formula is
+  // monotone in the box bounds when 1/d is finite), so the root node need not
+  // be fetched. Used only when all three 1/d components are finite.
+  float rbox[6];
 };
 
-__device__ __forceinline__ void tri_test(const rtl::GTri *__restrict__ tris, uint32_t k, f3 o, f3 d,
-                                         float &best, uint32_t &best_k) {
-  // triangle_intersection (ray_pack.ispc:132-165); e1/e2 precomputed (exact)
-  const float4 *q = reinterpret_cast<const float4 *>(tris + k);
-  const float4 a = q[0], b = q[1], c = q[2];
+// triangle_intersection (ray_pack.ispc:132-165) on one triangle already in
+// registers (v0, e1 = v1-v0, e2 = v2-v0; the subtractions are exact host-side
+// float ops, identical to the reference's). Returns t, or +inf on a miss.
+__device__ __forceinline__ float tri_t(float4 a, float4 b, float4 c, f3 o, f3 d) {
   const f3 v0{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
   const f3 pvec = cross(d, e2);
   const float det = dot(e1, pvec);
-  if (det < 1e-8f && det > -1e-8f) return;
   const float inv_det = 1 / det;
   const f3 tvec = o - v0;
   const float u = dot(tvec, pvec) * inv_det;
-  if (u < 0.0f || u > 1.0f) return;
   const f3 qvec = cross(tvec, e1);
   const float v = dot(d, qvec) * inv_det;
-  if (v < 0.0f || u + v > 1.0f) return;
   const float t = dot(e2, qvec) * inv_det;
-  if (best > t) { best = t; best_k = k; }
+  const bool miss = (det < 1e-8f && det > -1e-8f) || u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f;
+  return miss ? kInf : t;
 }
 
 __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uint32_t k) {
@@ -79,7 +81,11 @@ __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uin
   return normalize(cross(f3{b.x, b.y, b.z}, f3{c.x, c.y, c.z}));
 }
 
-// One leaf: its local best (first wins among equal t, triangle order).
+// One leaf: its local best, first wins among equal t (strict `>` in triangle
+// order, triangles_raytracing.cpp:324-331). The leaf's triangles are read in
+// batches of 4 with all 12 loads in flight together (the triangle array is
+// padded by 8 entries, so reading past a short leaf is in bounds and the
+// extra lanes are discarded), instead of one memory round trip per triangle.
 template <class CT>
 __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, uint32_t w, f3 o,
                                           f3 d, float &lt, uint32_t &lk, CT &cnt) {
@@ -87,14 +93,31 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
   const uint32_t n = (w & 7u) + 1u;
   cnt.add(C_BVH_LEAF, 1);
   cnt.add(C_BVH_TRI, n);
-  for (uint32_t k = 0; k < n; ++k) tri_test(tris, first + k, o, d, lt, lk);
+  const float4 *q = reinterpret_cast<const float4 *>(tris + first);
+  for (uint32_t base = 0; base < n; base += 4) {
+    float4 a[4], b[4], c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = q[3 * (base + k)];
+      b[k] = q[3 * (base + k) + 1];
+      c[k] = q[3 * (base + k) + 2];
+    }
+    float tk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tk[k] = tri_t(a[k], b[k], c[k], o, d);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (base + k < n && lt > tk[k]) { lt = tk[k]; lk = first + base + k; }
+  }
 }
 
 // Expand an inner node: slab-test its 8 children, sort8, keep t >= 0 entries
-// (a suffix of the sorted order) as a packed list of 3-bit ids + count.
+// (a suffix of the sorted order) as a packed list of 3-bit ids + count. Also
+// returns the entry distance and child word of the first child to visit (the
+// child words arrive with the boxes: descending needs no extra load).
 __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node, f3 o, f3 inv,
                                             float tNear, float tFar, uint32_t &list,
-                                            uint32_t &cnt, float &tfirst) {
+                                            uint32_t &cnt, float &tfirst, uint32_t &cwfirst) {
   const float4 *p = reinterpret_cast<const float4 *>(node);
   float bx[48];
 #pragma unroll
@@ -102,6 +125,9 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
     const float4 v = p[i];
     bx[4 * i] = v.x; bx[4 * i + 1] = v.y; bx[4 * i + 2] = v.z; bx[4 * i + 3] = v.w;
   }
+  const uint4 cw0 = reinterpret_cast<const uint4 *>(node->child)[0];
+  const uint4 cw1 = reinterpret_cast<const uint4 *>(node->child)[1];
+  const uint32_t cws[8] = {cw0.x, cw0.y, cw0.z, cw0.w, cw1.x, cw1.y, cw1.z, cw1.w};
   float t[8];
   uint32_t id[8];
 #pragma unroll
@@ -114,39 +140,72 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
   list = 0;
   cnt = 0;
   tfirst = 0.0f;
+  uint32_t first_id = 0;
 #pragma unroll
   for (int i = 7; i >= 0; --i) {  // build from the back so the first visit ends in the low bits
     if (!(t[i] < 0.0f)) {
       list = (list << 3) | id[i];
       cnt += 1;
       tfirst = t[i];
+      first_id = id[i];
     }
   }
+  uint32_t cf = cws[0];
+#pragma unroll
+  for (int c = 1; c < 8; ++c) cf = (first_id == (uint32_t)c) ? cws[c] : cf;
+  cwfirst = cf;
 }
 
-template <int BLOCK>
+template <int BLOCK, int F = 3>
 struct LdsStack {
-  uint32_t *base;  // lane-interleaved words
+  uint32_t *base;  // lane-interleaved words, F words per frame slot
   __device__ __forceinline__ uint32_t &at(int slot, int field) {
-    return base[(slot * 3 + field) * BLOCK];
+    return base[(slot * F + field) * BLOCK];
   }
 };
 
 // ANY = true: shadow-ray query, stop at the first leaf hit (only hitten is used).
+// Slab test of the root union box: true iff the ray certainly misses it.
+__device__ __forceinline__ bool root_box_miss(const float *b, f3 o, f3 inv, float tNear, float tFar) {
+  if (!(__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z)))
+    return false;  // 1/d = inf: NaN slabs possible, take the exact path
+  const float t1x = (b[0] - o.x) * inv.x, t1y = (b[1] - o.y) * inv.y, t1z = (b[2] - o.z) * inv.z;
+  const float t2x = (b[3] - o.x) * inv.x, t2y = (b[4] - o.y) * inv.y, t2z = (b[5] - o.z) * inv.z;
+  float tMin = isp_max(isp_min(t1x, t2x), isp_max(isp_min(t1y, t2y), isp_min(t1z, t2z)));
+  float tMax = isp_min(isp_max(t1x, t2x), isp_min(isp_max(t1y, t2y), isp_max(t1z, t2z)));
+  tMin = isp_max(tMin, tNear);
+  tMax = isp_min(tMax, tFar);
+  return tMax < 0.0f || tMin > tMax;
+}
+
+// Root stage of BVHBuilder::traverseNode(0): the union-box pretest and the
+// root's 8-child expansion (wave-uniform node: scalar loads). Returns false if
+// the traversal ends here (no child entered); otherwise the root frame.
+template <class CT>
+__device__ __forceinline__ bool mesh_root(const MeshDev &sc, f3 o, f3 inv, float tNear, float tFar,
+                                          uint32_t &l, uint32_t &c, float &tf, uint32_t &cwf,
+                                          CT &cnt) {
+  cnt.add(C_BVH_INNER, 1);
+  if (root_box_miss(sc.rbox, o, inv, tNear, tFar)) return false;
+  expand_node(sc.nodes + sc.root, o, inv, tNear, tFar, l, c, tf, cwf);
+  return c != 0;
+}
+
+// Traversal below the root frame (or from a root leaf when root_is_leaf).
 template <int BLOCK, bool ANY, class CT>
-__device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                           LdsStack<BLOCK> st, float &out_t, uint32_t &out_k,
-                                           CT &cnt) {
-  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
+__device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear,
+                                              float tFar, LdsStack<BLOCK> st, uint32_t word,
+                                              uint32_t flist, uint32_t fcnt, float tnext,
+                                              uint32_t cwnext, bool have_t, int depth,
+                                              float &out_t, uint32_t &out_k, CT &cnt) {
   float gbest = kInf;
   uint32_t gk = rtl::kInvalidChild;
-  uint32_t word = sc.root;
   // top frame in registers; frames below it in LDS slots [0, depth-2]
-  uint32_t fnode = 0, flist = 0, fcnt = 0;
+  uint32_t fnode = sc.root;
   float fbest = kInf;
-  int depth = 0;
-  float tnext = 0.0f;
-  bool have_t = false;
+  // One loop iteration = one unit of this lane's work (expand a node, test a
+  // leaf, or resume/pop a frame). (Measured and rejected: the "while-while"
+  // split into an inner-node phase and a leaf phase: bunny 0.342 -> 0.523 ms.)
   for (;;) {
     if (word != rtl::kInvalidChild) {
       if (word & rtl::kLeafBit) {
@@ -159,10 +218,10 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
           if (lt < gbest) { gbest = lt; gk = lk; }
         }
       } else {
-        uint32_t l, c;
+        uint32_t l, c, cwf;
         float tf;
         cnt.add(C_BVH_INNER, 1);
-        expand_node(sc.nodes + word, o, inv, tNear, tFar, l, c, tf);
+        expand_node(sc.nodes + word, o, inv, tNear, tFar, l, c, tf, cwf);
         if (c != 0) {
           if (depth >= 1) {
             st.at(depth - 1, 0) = fnode;
@@ -172,6 +231,7 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
           ++depth;
           fnode = word; flist = l; fcnt = c; fbest = kInf;
           tnext = tf;
+          cwnext = cwf;
           have_t = true;
         }
       }
@@ -194,18 +254,35 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
     const uint32_t j = flist & 7u;
     flist >>= 3;
     fcnt -= 1;
-    const rtl::GNode *nd = sc.nodes + fnode;
-    if (!have_t) {
+    if (!have_t) {  // resumed frame: child box and word, loaded together
+      const rtl::GNode *nd = sc.nodes + fnode;
       const float *b = nd->box[j];
+      cwnext = nd->child[j];
       tnext = slab_ispc(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
     }
     have_t = false;
     if (fbest < tnext) { fcnt = 0; continue; }  // pruned; later siblings have larger t
-    word = nd->child[j];
+    word = cwnext;
   }
   out_t = gbest;
   out_k = gk;
   return gk != rtl::kInvalidChild;
+}
+
+template <int BLOCK, bool ANY, class CT>
+__device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
+                                           LdsStack<BLOCK> st, float &out_t, uint32_t &out_k,
+                                           CT &cnt) {
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
+  if (sc.root == rtl::kInvalidChild) return false;
+  if (sc.root & rtl::kLeafBit)
+    return mesh_continue<BLOCK, ANY>(sc, o, d, inv, tNear, tFar, st, sc.root, 0u, 0u, 0.0f,
+                                     rtl::kInvalidChild, false, 0, out_t, out_k, cnt);
+  uint32_t l, c, cwf;
+  float tf;
+  if (!mesh_root(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)) return false;
+  return mesh_continue<BLOCK, ANY>(sc, o, d, inv, tNear, tFar, st, rtl::kInvalidChild, l, c, tf, cwf,
+                                   true, 1, out_t, out_k, cnt);
 }
 
 template <int BLOCK, class CT>
@@ -345,19 +422,24 @@ struct OctDev {
 };
 
 __device__ __forceinline__ void oct_box(uint32_t ix, uint32_t iy, uint32_t iz, int depth, f3 &bmin,
-                                        f3 &bmax) {
+                                        f3 &bmax, float &inv_s) {
   const float s = __builtin_ldexpf(2.0f, -depth);
   bmin = f3{-1.0f + (float)ix * s, -1.0f + (float)iy * s, -1.0f + (float)iz * s};
   bmax = f3{bmin.x + s, bmin.y + s, bmin.z + s};
+  inv_s = __builtin_ldexpf(0.5f, depth);
 }
 
 struct OctCorners {
   float v[8];
 };
 
-__device__ __forceinline__ void oct_local(f3 bmin, f3 bmax, f3 p, f3 &a, f3 &b) {
-  // point = (p - boxMin) / (boxMax - boxMin); clamp to [1e-7, 0.9999999]
-  p = (p - bmin) / (bmax - bmin);
+// point = (p - boxMin) / (boxMax - boxMin), clamped to [1e-7, 0.9999999]
+// (octree_raytracing.cpp:24-25). boxMax - boxMin is exactly the node size s, a
+// power of two (exact dyadic box arithmetic), and x / 2^k == x * 2^-k bit for
+// bit (both round the exact value once, subnormals included), so the three
+// divisions become multiplications by inv_s = 1/s.
+__device__ __forceinline__ void oct_local(f3 bmin, float inv_s, f3 p, f3 &a, f3 &b) {
+  p = (p - bmin) * inv_s;
   p = vstd_min(vstd_max(p, f3{0.0000001f, 0.0000001f, 0.0000001f}),
                f3{0.9999999f, 0.9999999f, 0.9999999f});
   const f3 c0{__builtin_floorf(p.x), __builtin_floorf(p.y), __builtin_floorf(p.z)};
@@ -366,9 +448,9 @@ __device__ __forceinline__ void oct_local(f3 bmin, f3 bmax, f3 p, f3 &a, f3 &b) 
   b = c1 - p;  // c1f_p
 }
 
-__device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, f3 bmax, f3 p) {
+__device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, float inv_s, f3 p) {
   f3 a, b;
-  oct_local(bmin, bmax, p, a, b);
+  oct_local(bmin, inv_s, p, a, b);
   float res = 0.0f;  // octree_raytracing.cpp:36-55, values[(x<<2)+(y<<1)+z]
   res += c.v[0] * b.x * b.y * b.z;
   res += c.v[1] * b.x * b.y * a.z;
@@ -381,9 +463,9 @@ __device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, f3 bmax, 
   return res;
 }
 
-__device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, f3 bmax, f3 p) {
+__device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, float inv_s, f3 p) {
   f3 a, b;
-  oct_local(bmin, bmax, p, a, b);
+  oct_local(bmin, inv_s, p, a, b);
   const float da = 1.0f, db = -1.0f;  // dp_c0f, dc1f_p (octree_raytracing.cpp:79-80)
   const float *v = c.v;
   const float dfdx = v[0] * db * b.y * b.z + v[1] * db * b.y * a.z + v[2] * db * a.y * b.z +
@@ -400,9 +482,9 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, f3 bmax, 
 
 // intersectLeaf (octree_raytracing.cpp:122-164) for a leaf that may hit.
 template <bool NEED_NORMAL, class CT>
-__device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax, f3 o,
-                                         f3 d, f3 inv, float tNear, float tFar, float &out_t,
-                                         f3 &out_n, CT &cnt) {
+__device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax,
+                                         float inv_s, f3 o, f3 d, f3 inv, float tNear, float tFar,
+                                         float &out_t, f3 &out_n, CT &cnt) {
   float t1, t2;
   bbox_intersection(bmin, bmax, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
@@ -417,11 +499,11 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   p = vstd_min(p, bmax);
   while (p.x <= bmax.x && p.y <= bmax.y && p.z <= bmax.z && p.x >= bmin.x && p.y >= bmin.y &&
          p.z >= bmin.z) {
-    const float s = oct_sdf(c, bmin, bmax, p);
+    const float s = oct_sdf(c, bmin, inv_s, p);
     cnt.add(C_OCT_STEP, 1);
     if (s < 1e-4f) {
       out_t = t + s;
-      if (NEED_NORMAL) { out_n = oct_normal(c, bmin, bmax, p); cnt.add(C_OCT_NORMAL, 1); }
+      if (NEED_NORMAL) { out_n = oct_normal(c, bmin, inv_s, p); cnt.add(C_OCT_NORMAL, 1); }
       return true;
     }
     t += s;
@@ -431,19 +513,32 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
 }
 
 // Expand an octree inner node: divide_box_8 + intersect_box_8 + sort8, keep
-// entries with t > 0 (octree_raytracing.cpp:185).
+// entries with t > 0 (octree_raytracing.cpp:175-199). The 8 child boxes have
+// only 3 distinct bounds per axis (min, centre, max: centre + diff == max and
+// min + diff == centre exactly), so the 24 slab distances of the reference
+// are 9 distinct values, computed once each with the reference's operations.
 __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar,
                                            uint32_t &list, uint32_t &cnt) {
   const f3 center{(bmin.x + bmax.x) / 2.0f, (bmin.y + bmax.y) / 2.0f, (bmin.z + bmax.z) / 2.0f};
   const f3 diff = center - bmin;
+  const f3 hi{center.x + diff.x, center.y + diff.y, center.z + diff.z};  // == bmax, the child max
+  const float x0 = (bmin.x - o.x) * inv.x, x1 = (center.x - o.x) * inv.x, x2 = (hi.x - o.x) * inv.x;
+  const float y0 = (bmin.y - o.y) * inv.y, y1 = (center.y - o.y) * inv.y, y2 = (hi.y - o.y) * inv.y;
+  const float z0 = (bmin.z - o.z) * inv.z, z1 = (center.z - o.z) * inv.z, z2 = (hi.z - o.z) * inv.z;
+  // per axis and half: (min, max) of the two slab distances, ISPC operand order
+  const float mnx[2] = {isp_min(x0, x1), isp_min(x1, x2)}, mxx[2] = {isp_max(x0, x1), isp_max(x1, x2)};
+  const float mny[2] = {isp_min(y0, y1), isp_min(y1, y2)}, mxy[2] = {isp_max(y0, y1), isp_max(y1, y2)};
+  const float mnz[2] = {isp_min(z0, z1), isp_min(z1, z2)}, mxz[2] = {isp_max(z0, z1), isp_max(z1, z2)};
   float t[8];
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int x = c >> 2, y = (c & 3) >> 1, z = c & 1;
-    const float x0 = x == 0 ? bmin.x : center.x, y0 = y == 0 ? bmin.y : center.y,
-                z0 = z == 0 ? bmin.z : center.z;
-    t[c] = slab_ispc(x0, y0, z0, x0 + diff.x, y0 + diff.y, z0 + diff.z, o, inv, tNear, tFar);
+    float tMin = isp_max(mnx[x], isp_max(mny[y], mnz[z]));
+    float tMax = isp_min(mxx[x], isp_min(mxy[y], mxz[z]));
+    tMin = isp_max(tMin, tNear);
+    tMax = isp_min(tMax, tFar);
+    t[c] = (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
     id[c] = (uint32_t)c;
   }
   sort8(t, id);
@@ -460,7 +555,7 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
 
 template <int BLOCK, bool NEED_NORMAL, class CT>
 __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                          LdsStack<BLOCK> st, float &out_t, f3 &out_n,
+                                          LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
                                           uint32_t &out_node, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   const uint32_t root = sc.child[0];
@@ -469,8 +564,8 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
     cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return false;
     out_node = 0;
-    return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, d, inv,
-                                 tNear, tFar, out_t, out_n, cnt);
+    return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d,
+                                 inv, tNear, tFar, out_t, out_n, cnt);
   }
   // top frame: node whose children are being visited, its coords and list
   uint32_t fnode = 0, flist, fcnt;
@@ -478,7 +573,8 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
   int depth = 0;  // depth of fnode (root = 0); frames below the top live in LDS
   {
     f3 bmin, bmax;
-    oct_box(0, 0, 0, 0, bmin, bmax);
+    float inv_s;
+    oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
     oct_expand(bmin, bmax, o, inv, tNear, tFar, flist, fcnt);
   }
   for (;;) {
@@ -501,10 +597,12 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
     cnt.add(C_OCT_NODE, 1);
     if (cw == rtl::kOctNeverHits) { cnt.add(C_OCT_LEAF, 1); continue; }
     f3 bmin, bmax;
-    oct_box(cx, cy, cz, depth + 1, bmin, bmax);
+    float inv_s;
+    oct_box(cx, cy, cz, depth + 1, bmin, bmax, inv_s);
     if (cw == 0) {
       cnt.add(C_OCT_LEAF, 1);
-      if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, o, d, inv, tNear, tFar, out_t, out_n, cnt)) {
+      if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, out_n,
+                                cnt)) {
         out_node = cn;
         return true;
       }
@@ -523,7 +621,7 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
 
 template <int BLOCK, class CT>
 __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK> st, CT &cnt) {
+                                             LdsStack<BLOCK, 2> st, CT &cnt) {
   Hit h = miss_hit();
   uint32_t node;
   if (oct_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, h.t, h.n, node, cnt)) {
@@ -536,7 +634,7 @@ __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float
 }
 template <int BLOCK, class CT>
 __device__ __forceinline__ bool oct_occluded(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK> st, CT &cnt) {
+                                             LdsStack<BLOCK, 2> st, CT &cnt) {
   float t;
   f3 n;
   uint32_t node;

@@ -11,7 +11,7 @@ import os
 import subprocess
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "librtamd.so")
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(PKG_ROOT, "lib", "librtamd.so")
 
 RT_OK = 0
 RT_FLAG_CLEAR = 1
