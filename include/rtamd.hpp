@@ -1,0 +1,266 @@
+// rtamd.hpp -- header-only C++ mirror of the reference's render surface over
+// the C ABI in rtamd.h. A user of iMacsimus/Triangles-SDF-CPU-RayTracing can
+// keep the shape of their code:
+//
+//   reference (src/...)                            here (namespace rtamd)
+//   --------------------------------------------   ------------------------------------
+//   cmesh4::LoadMeshFromObj + loadAndScale          LoadMeshFromObj(path, /*scale=*/true)
+//   BVHBuilder b; b.perform(std::move(mesh));       BVHBuilder b; b.perform(mesh);
+//   SDFGrid g; loadSDFGrid(g, path);                SDFGrid g; loadSDFGrid(g, path);
+//   SDFOctree o; loadSDFOctree(o, path);            SDFOctree o; loadSDFOctree(o, path);
+//   Plane(float3{0,1,0}, y)                         Plane{{0,1,0}, y}
+//   SceneUnion(scene, plane)                        SceneUnion(scene, plane)
+//   Camera(pos, target, up)                         Camera(pos, target, up)
+//   FrameBuffer fb; fb.resize(W,H); fb.clear();     FrameBuffer fb; fb.resize(W,H); fb.clear();
+//   inverse4x4(perspectiveMatrix(45, W/H, .01,100)) projInverse(45, W/H, .01, 100)
+//   renderer.draw(scene, fb, camera, projInv)       renderer.draw(scene, fb, camera, projInv)
+//   IScene::intersect(o, d, tNear, tFar)            scene.intersect(o, d, tNear, tFar)
+//
+// (raytracing.hpp:9-213, triangles_raytracing.hpp:38-67, grid_raytracing.hpp,
+// octree_raytracing.hpp, camera.hpp, main.cpp:198-206.) Everything runs on the
+// current HIP device through librtamd.so; errors throw rtamd::Error.
+#pragma once
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "rtamd.h"
+
+namespace rtamd {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+inline void check(int rc) {
+  if (rc != RT_OK) throw Error(rc, std::string("rtamd: ") + rt_last_error());
+}
+
+struct float3 {
+  float x = 0, y = 0, z = 0;
+};
+using float4x4 = std::array<float, 16>;  // column-major, LiteMath m_col layout
+
+enum class ShadingMode { Normal = RT_SHADING_NORMAL, Lambert = RT_SHADING_LAMBERT, Color = RT_SHADING_COLOR };
+
+// HitInfo (raytracing.hpp:67-73) + this build's primitive id.
+struct HitInfo {
+  bool hitten = false;
+  float t = 0.0f;
+  float3 normal{0.0f, 1.0f, 0.0f};
+  int64_t prim = -1;
+};
+
+struct SimpleMesh {  // cmesh4::SimpleMesh positions + indices (core/mesh.h:15-55)
+  std::vector<float> vPos4f;      // 4 floats per vertex
+  std::vector<uint32_t> indices;  // 3 per triangle
+  size_t TrianglesNum() const { return indices.size() / 3; }
+};
+
+inline SimpleMesh LoadMeshFromObj(const std::string &path, bool scale = true) {
+  int64_t nv = 0, ni = 0;
+  check(rt_load_obj(path.c_str(), scale ? 1 : 0, nullptr, &nv, nullptr, &ni));
+  SimpleMesh m;
+  m.vPos4f.resize((size_t)nv * 4);
+  m.indices.resize((size_t)ni);
+  check(rt_load_obj(path.c_str(), scale ? 1 : 0, m.vPos4f.data(), &nv, m.indices.data(), &ni));
+  return m;
+}
+
+// FrameBuffer {Image2D<uint32_t> color; Image2D<float> t;} (raytracing.hpp:9-20)
+struct FrameBuffer {
+  std::vector<uint32_t> color;
+  std::vector<float> t;
+  uint32_t w = 0, h = 0;
+  void resize(uint32_t width, uint32_t height) {
+    w = width;
+    h = height;
+    color.assign((size_t)w * h, 0u);
+    t.assign((size_t)w * h, std::numeric_limits<float>::infinity());
+  }
+  void clear() {
+    std::fill(color.begin(), color.end(), 0u);
+    std::fill(t.begin(), t.end(), std::numeric_limits<float>::infinity());
+  }
+  uint32_t width() const { return w; }
+  uint32_t height() const { return h; }
+};
+
+// Camera (camera.hpp:7-61): position / target / up; the view matrix is the
+// reference's lookAt of its quaternion-derived up vector.
+class Camera {
+ public:
+  Camera() = default;
+  Camera(float3 position, float3 target, float3 up = {0.0f, 1.0f, 0.0f})
+      : pos_(position), target_(target), up_(up) {}
+  float3 position() const { return pos_; }
+  float3 target() const { return target_; }
+  // inverse4x4(lookAtMatrix())
+  float4x4 viewInverse() const {
+    float4x4 vi{}, pi{};
+    const float p[3] = {pos_.x, pos_.y, pos_.z}, t[3] = {target_.x, target_.y, target_.z},
+                u[3] = {up_.x, up_.y, up_.z};
+    check(rt_camera(p, t, u, 45.0f, 1.0f, 0.01f, 100.0f, vi.data(), pi.data()));
+    return vi;
+  }
+
+ private:
+  float3 pos_{0.0f, 0.0f, 2.5f}, target_{}, up_{0.0f, 1.0f, 0.0f};
+};
+
+// inverse4x4(perspectiveMatrix(fovy, aspect, zNear, zFar)) (main.cpp:198-201)
+inline float4x4 projInverse(float fovy, float aspect, float znear, float zfar) {
+  float4x4 vi{}, pi{};
+  const float p[3] = {0, 0, 1}, t[3] = {0, 0, 0}, u[3] = {0, 1, 0};
+  check(rt_camera(p, t, u, fovy, aspect, znear, zfar, vi.data(), pi.data()));
+  return pi;
+}
+
+struct Plane {  // Plane(normal, offset): dot(p, normal) = offset (raytracing.hpp:121-124)
+  float3 normal{0.0f, 1.0f, 0.0f};
+  float offset = 0.0f;
+};
+
+// A scene resident on the current HIP device (IScene, raytracing.hpp:75-81).
+class IScene {
+ public:
+  IScene() = default;
+  IScene(const IScene &) = delete;
+  IScene &operator=(const IScene &) = delete;
+  virtual ~IScene() = default;
+
+  rt_scene *handle() const {
+    if (!h_) throw Error(RT_E_STATE, "rtamd: scene not built");
+    return h_.get();
+  }
+  // IScene::intersect for one ray (for many rays use intersect(n, ...)).
+  HitInfo intersect(float3 o, float3 d, float tNear, float tFar) const {
+    HitInfo r;
+    intersect(1, &o.x, &d.x, tNear, tFar, &r);
+    return r;
+  }
+  void intersect(int64_t n, const float *o3, const float *d3, float tNear, float tFar, HitInfo *out) const {
+    std::vector<int32_t> hit((size_t)n);
+    std::vector<float> t((size_t)n), nrm((size_t)n * 3);
+    std::vector<int64_t> prim((size_t)n);
+    check(rt_intersect_rays(handle(), o3, d3, n, tNear, tFar, hit.data(), t.data(), nrm.data(), prim.data()));
+    for (int64_t i = 0; i < n; ++i)
+      out[i] = HitInfo{hit[(size_t)i] != 0, t[(size_t)i],
+                       {nrm[3 * (size_t)i], nrm[3 * (size_t)i + 1], nrm[3 * (size_t)i + 2]}, prim[(size_t)i]};
+  }
+  void setPlane(const Plane *p) const {
+    const float n[3] = {p ? p->normal.x : 0.0f, p ? p->normal.y : 1.0f, p ? p->normal.z : 0.0f};
+    check(rt_scene_set_plane(handle(), p ? 1 : 0, n, p ? p->offset : 0.0f));
+  }
+
+ protected:
+  struct Del {
+    void operator()(rt_scene *s) const { rt_scene_destroy(s); }
+  };
+  void reset(rt_scene *s) { h_.reset(s); }
+  std::unique_ptr<rt_scene, Del> h_;
+};
+
+// BVHBuilder::perform (triangles_raytracing.cpp:227-258): same SAH BVH8.
+class BVHBuilder : public IScene {
+ public:
+  void perform(const SimpleMesh &mesh) {
+    rt_scene *s = nullptr;
+    check(rt_scene_create_mesh(mesh.vPos4f.data(), (int64_t)(mesh.vPos4f.size() / 4), mesh.indices.data(),
+                               (int64_t)mesh.indices.size(), &s));
+    reset(s);
+  }
+  size_t nodesCount() const {
+    int64_t n = 0, inner = 0;
+    int32_t d = 0;
+    check(rt_scene_bvh_stats(handle(), &n, &inner, &d));
+    return (size_t)n;
+  }
+};
+
+class SDFGrid : public IScene {  // grid_raytracing.hpp:10-21
+ public:
+  uint32_t size[3] = {0, 0, 0};
+  std::vector<float> values;  // host copy, x-major (x*sy+y)*sz+z
+  void upload() {
+    rt_scene *s = nullptr;
+    check(rt_scene_create_grid(size, values.data(), &s));
+    reset(s);
+  }
+};
+inline void loadSDFGrid(SDFGrid &g, const std::string &path) {  // grid_raytracing.cpp:127-134
+  check(rt_load_grid(path.c_str(), g.size, nullptr));
+  g.values.resize((size_t)g.size[0] * g.size[1] * g.size[2]);
+  check(rt_load_grid(path.c_str(), g.size, g.values.data()));
+  g.upload();
+}
+
+class SDFOctree : public IScene {  // octree_raytracing.hpp:20-47
+ public:
+  std::vector<uint8_t> nodes;  // count x 36-byte SDFOctreeNode
+  void upload() {
+    rt_scene *s = nullptr;
+    check(rt_scene_create_octree(nodes.data(), (int64_t)(nodes.size() / 36), &s));
+    reset(s);
+  }
+};
+inline void loadSDFOctree(SDFOctree &o, const std::string &path) {  // octree_raytracing.cpp:8-16
+  int64_t n = 0;
+  check(rt_load_octree(path.c_str(), &n, nullptr));
+  o.nodes.resize((size_t)n * 36);
+  check(rt_load_octree(path.c_str(), &n, o.nodes.data()));
+  o.upload();
+}
+
+// SceneUnion(scene, plane) (raytracing.hpp:83-97): the reference application
+// only ever unions a scene with the ground plane (main.cpp:64, 190).
+struct SceneUnion {
+  const IScene &first;
+  Plane second;
+  SceneUnion(const IScene &a, Plane p) : first(a), second(p) {}
+};
+
+// Renderer (raytracing.hpp:101-117).
+struct Renderer {
+  float3 lightPos{2.0f, 2.0f, 2.0f};  // main.cpp:60
+  bool enableShadows = true;
+  bool enableReflections = true;
+  ShadingMode shadingMode = ShadingMode::Lambert;
+
+  // Renderer::draw: t is read as tPrev, pixels written only on hit
+  // (raytracing.cpp:67-102). Returns the kernel time in milliseconds.
+  float draw(const IScene &scene, FrameBuffer &fb, const Camera &camera, const float4x4 &projInv) const {
+    scene.setPlane(nullptr);
+    return drawImpl(scene, fb, camera, projInv);
+  }
+  float draw(const SceneUnion &u, FrameBuffer &fb, const Camera &camera, const float4x4 &projInv) const {
+    u.first.setPlane(&u.second);
+    return drawImpl(u.first, fb, camera, projInv);
+  }
+
+ private:
+  float drawImpl(const IScene &scene, FrameBuffer &fb, const Camera &camera, const float4x4 &projInv) const {
+    rt_render_params p{};
+    const float3 c = camera.position();
+    p.camera_pos[0] = c.x; p.camera_pos[1] = c.y; p.camera_pos[2] = c.z;
+    const float4x4 vi = camera.viewInverse();
+    for (int i = 0; i < 16; ++i) { p.view_inv[i] = vi[(size_t)i]; p.proj_inv[i] = projInv[(size_t)i]; }
+    p.light_pos[0] = lightPos.x; p.light_pos[1] = lightPos.y; p.light_pos[2] = lightPos.z;
+    p.shading_mode = (int32_t)shadingMode;
+    p.enable_shadows = enableShadows;
+    p.enable_reflections = enableReflections;
+    float ms = 0.0f;
+    check(rt_render(scene.handle(), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
+                    (int32_t)fb.height(), 0u, &ms));
+    return ms;
+  }
+};
+
+}  // namespace rtamd
