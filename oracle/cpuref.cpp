@@ -41,6 +41,8 @@
 #include <string>
 #include <unordered_map>
 #include <utility>
+#include <array>
+#include <map>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
@@ -971,6 +973,128 @@ struct RefParams {
 
 static Counters g_cnt;
 
+
+// ---------------------------------------------------------------------------
+// Mesh -> signed distance. The reference has no SDF
+// generator; this is the definition the GPU construction
+// (triangles-sdf-cpu-raytracing_amd/csrc/rt_sdfgen.hip) must reproduce bit for
+// bit, stated by BRUTE FORCE (every triangle, original order, strictly smaller
+// d^2 wins, so ties keep the lowest triangle id):
+//   closest point + Voronoi region: Ericson, Real-Time Collision Detection
+//   5.1.5 (ClosestPtPointTriangle), regions 0..2 vertex a,b,c, 3 ab, 4 ac,
+//   5 bc, 6 face; sign: angle-weighted pseudonormal (Baerentzen & Aanaes)
+//   of that feature, over vertices welded by exact position bits, accumulated
+//   in double in triangle order; negative iff dot(p - q, N) < 0.
+// Parity of this definition is "unpinned" against the reference (it has no
+// such function); it pins the GPU generator only.
+namespace sdfref {
+struct Feat { float3 q; int f; };
+static Feat closest(float3 p, float3 a, float3 b, float3 c) {
+  float3 ab = b - a, ac = c - a, ap = p - a;
+  float d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.0f && d2 <= 0.0f) return {a, 0};
+  float3 bp = p - b;
+  float d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.0f && d4 <= d3) return {b, 1};
+  float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0f && d1 >= 0.0f && d3 <= 0.0f) { float v = d1 / (d1 - d3); return {a + ab * v, 3}; }
+  float3 cp = p - c;
+  float d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0.0f && d5 <= d6) return {c, 2};
+  float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) { float w = d2 / (d2 - d6); return {a + ac * w, 4}; }
+  float va = d3 * d6 - d5 * d4;
+  if (va <= 0.0f && (d4 - d3) >= 0.0f && (d5 - d6) >= 0.0f) {
+    float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    return {b + (c - b) * w, 5};
+  }
+  float denom = 1.0f / (va + vb + vc);
+  float v = vb * denom, w = vc * denom;
+  return {a + ab * v + ac * w, 6};
+}
+struct Mesh {
+  std::vector<float3> tv;   // 3 per triangle
+  std::vector<float3> pn;   // 7 per triangle
+};
+static void prepare(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, Mesh &m) {
+  const size_t ntri = (size_t)nidx / 3;
+  std::vector<float3> P((size_t)nverts);
+  for (int64_t v = 0; v < nverts; ++v)
+    P[(size_t)v] = float3(vpos4[4 * v] / vpos4[4 * v + 3], vpos4[4 * v + 1] / vpos4[4 * v + 3],
+                          vpos4[4 * v + 2] / vpos4[4 * v + 3]);
+  std::map<std::array<uint32_t, 3>, uint32_t> wm;
+  std::vector<uint32_t> weld((size_t)nverts);
+  for (int64_t v = 0; v < nverts; ++v) {
+    std::array<uint32_t, 3> k;
+    std::memcpy(k.data(), (const void *)&P[(size_t)v], 12);
+    auto it = wm.find(k);
+    if (it == wm.end()) it = wm.emplace(k, (uint32_t)wm.size()).first;
+    weld[(size_t)v] = it->second;
+  }
+  std::vector<std::array<double, 3>> va(wm.size(), {0.0, 0.0, 0.0});
+  std::map<std::pair<uint32_t, uint32_t>, std::array<double, 3>> ea;
+  std::vector<float3> fn(ntri);
+  auto ek = [&](uint32_t a, uint32_t b) {
+    return std::make_pair(std::min(weld[a], weld[b]), std::max(weld[a], weld[b]));
+  };
+  for (size_t t = 0; t < ntri; ++t) {
+    const uint32_t *vi = idx + 3 * t;
+    float3 a = P[vi[0]], b = P[vi[1]], c = P[vi[2]];
+    float3 n = cross(b - a, c - a);
+    float l = std::sqrt(dot(n, n));
+    float3 nf = l > 0.0f ? float3(n.x / l, n.y / l, n.z / l) : float3(0.0f);
+    fn[t] = nf;
+    const float3 corner[3] = {a, b, c};
+    for (int k = 0; k < 3; ++k) {
+      float3 o = corner[k], u = corner[(k + 1) % 3], w = corner[(k + 2) % 3];
+      double u0 = (double)u.x - o.x, u1 = (double)u.y - o.y, u2 = (double)u.z - o.z;
+      double w0 = (double)w.x - o.x, w1 = (double)w.y - o.y, w2 = (double)w.z - o.z;
+      double lu = std::sqrt(u0 * u0 + u1 * u1 + u2 * u2), lw = std::sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+      double ang = 0.0;
+      if (lu > 0.0 && lw > 0.0) ang = std::acos(std::min(1.0, std::max(-1.0, (u0 * w0 + u1 * w1 + u2 * w2) / (lu * lw))));
+      auto &acc = va[weld[vi[k]]];
+      acc[0] += ang * nf.x; acc[1] += ang * nf.y; acc[2] += ang * nf.z;
+    }
+    for (auto key : {ek(vi[0], vi[1]), ek(vi[0], vi[2]), ek(vi[1], vi[2])}) {
+      auto &e = ea[key];
+      e[0] += nf.x; e[1] += nf.y; e[2] += nf.z;
+    }
+  }
+  m.tv.resize(ntri * 3);
+  m.pn.resize(ntri * 7);
+  for (size_t t = 0; t < ntri; ++t) {
+    const uint32_t *vi = idx + 3 * t;
+    for (int k = 0; k < 3; ++k) {
+      m.tv[3 * t + k] = P[vi[k]];
+      const auto &acc = va[weld[vi[k]]];
+      m.pn[7 * t + k] = float3((float)acc[0], (float)acc[1], (float)acc[2]);
+    }
+    const std::pair<uint32_t, uint32_t> keys[3] = {ek(vi[0], vi[1]), ek(vi[0], vi[2]), ek(vi[1], vi[2])};
+    for (int k = 0; k < 3; ++k) {
+      const auto &e = ea.at(keys[k]);
+      m.pn[7 * t + 3 + k] = float3((float)e[0], (float)e[1], (float)e[2]);
+    }
+    m.pn[7 * t + 6] = fn[t];
+  }
+}
+static float query(const Mesh &m, float3 p) {
+  float best = INFINITY;
+  size_t bt = 0;
+  Feat bf{float3(0.0f), 0};
+  for (size_t t = 0; t < m.tv.size() / 3; ++t) {
+    Feat f = closest(p, m.tv[3 * t], m.tv[3 * t + 1], m.tv[3 * t + 2]);
+    float3 e = p - f.q;
+    float d2 = dot(e, e);
+    if (d2 < best) { best = d2; bt = t; bf = f; }
+  }
+  if (!(best < INFINITY)) return INFINITY;
+  float3 e = p - bf.q, N = m.pn[7 * bt + (size_t)bf.f];
+  float s = e.x * N.x + e.y * N.y + e.z * N.z;
+  float d = std::sqrt(best);
+  return s < 0.0f ? -d : d;
+}
+}  // namespace sdfref
+
 extern "C" {
 
 // Work counters accumulated by cpuref_render since the last reset:
@@ -1195,6 +1319,18 @@ uint64_t cpuref_fnv1a64(const uint32_t *c, int64_t n) {
   uint64_t h = 1469598103934665603ull;
   for (int64_t i = 0; i < n; ++i) h = (h ^ (uint64_t)c[i]) * 1099511628211ull;
   return h;
+}
+
+
+// Signed distance at n points (brute force; OpenMP over points).
+int cpuref_sdf_points(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, const float *p3,
+                      int64_t n, float *out, int nthreads) {
+  if (nidx <= 0 || nidx % 3) return -1;
+  sdfref::Mesh m;
+  sdfref::prepare(vpos4, nverts, idx, nidx, m);
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int64_t i = 0; i < n; ++i) out[i] = sdfref::query(m, float3(p3[3 * i], p3[3 * i + 1], p3[3 * i + 2]));
+  return 0;
 }
 
 }  // extern "C"

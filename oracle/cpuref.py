@@ -58,6 +58,7 @@ def lib():
         L.cpuref_pixel_cost.argtypes = [vp, vp, C.c_int, C.c_int, vp]
         L.cpuref_primary_rays.argtypes = [vp, C.c_int, C.c_int, vp]
         L.cpuref_fnv1a64.restype = C.c_uint64
+        L.cpuref_sdf_points.argtypes = [vp, i64, vp, i64, vp, i64, vp, C.c_int]
         L.cpuref_fnv1a64.argtypes = [vp, i64]
         _lib = L
     return _lib
@@ -225,3 +226,108 @@ def algorithmic_bytes(c: dict, pixels: int) -> int:
     return int(200 * c["bvh_inner"] + 8 * c["bvh_leaf"] + 60 * c["bvh_tri"] + 32 * c["grid_sdf"]
                + 4 * c["oct_node"] + 32 * c["oct_leaf"] + 32 * c["oct_step"] + 32 * c["oct_normal"]
                + 8 * pixels)
+
+
+# ------------------------------------------------------------ mesh -> SDF --
+# Definition of the SDF construction the GPU generator (rt_sdf_mesh_*) must
+# reproduce; the reference has none, so this is
+# "parity unpinned" against the reference and pins the GPU path only.
+
+def sdf_points(vpos4, idx, p3, threads: int = 8) -> np.ndarray:
+    """Signed distance at points p3 [n,3], brute force over all triangles."""
+    v = np.ascontiguousarray(vpos4, np.float32)
+    i = np.ascontiguousarray(idx, np.uint32)
+    p = np.ascontiguousarray(p3, np.float32).reshape(-1, 3)
+    out = np.empty(len(p), np.float32)
+    rc = lib().cpuref_sdf_points(_p(v), len(v), _p(i), len(i), _p(p), len(p), _p(out), int(threads))
+    if rc != 0:
+        raise ValueError("cpuref_sdf_points failed")
+    return out
+
+
+def lattice_points(size) -> np.ndarray:
+    """Sample (i,j,k) of a size[0] x size[1] x size[2] lattice at 2*i/(n-1) - 1
+    per axis (f32 ops: mul, div, sub), in the SDFGrid index order
+    (x*sy+y)*sz+z (grid_raytracing.hpp:13-15)."""
+    axes = [np.float32(2.0) * np.arange(n, dtype=np.float32) / np.float32(n - 1) - np.float32(1.0)
+            for n in (int(size[0]), int(size[1]), int(size[2]))]
+    X, Y, Z = np.meshgrid(*axes, indexing="ij")
+    return np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1)
+
+
+def sdf_octree(vpos4, idx, depth: int, threads: int = 8) -> np.ndarray:
+    """Sparse SDF octree in the reference's 36-byte node format (octree_raytracing.hpp:8-18):
+    top-down from the root [-1,1]^3; a node at depth d < depth is refined iff
+    |sdf(centre)| <= sqrt(3) * 2^-d (f32 1.7320508 * 2^-d); refined nodes hold
+    zeros and childrenOffset; unrefined nodes are empty leaves (values 1000);
+    depth-`depth` nodes are leaves with the SDF at their 8 corners,
+    values[(x<<2)+(y<<1)+z] (octree_raytracing.hpp:35-37). BFS order, the 8
+    children of a node contiguous, child id (x<<2)|(y<<1)|z (divide_box_8)."""
+    levels = [[(0, 0, 0)]]
+    refine = []
+    for d in range(depth):
+        cur = levels[d]
+        half = np.float32(2.0 ** -d)
+        c = np.array(cur, np.int64)
+        centres = (2 * c + 1).astype(np.float32) * half - np.float32(1.0)
+        s = sdf_points(vpos4, idx, centres, threads)
+        r = np.abs(s) <= np.float32(1.7320508) * half
+        refine.append(r)
+        nxt = []
+        for (x, y, z), rr in zip(cur, r):
+            if rr:
+                for k in range(8):
+                    nxt.append((2 * x + (k >> 2), 2 * y + ((k >> 1) & 1), 2 * z + (k & 1)))
+        levels.append(nxt)
+    leaves = np.array(levels[depth], np.int64).reshape(-1, 3)
+    size = np.float32(2.0 ** (1 - depth))
+    corners = np.array([(k >> 2, (k >> 1) & 1, k & 1) for k in range(8)], np.int64)
+    pts = ((leaves[:, None, :] + corners[None]).astype(np.float32) * size - np.float32(1.0)).reshape(-1, 3)
+    cv = sdf_points(vpos4, idx, pts, threads).reshape(-1, 8) if len(pts) else np.zeros((0, 8), np.float32)
+    total = sum(len(L) for L in levels)
+    vals = np.zeros((total, 8), np.float32)
+    off = np.zeros(total, np.uint32)
+    base = 0
+    for d in range(depth + 1):
+        n = len(levels[d])
+        child = base + n
+        for j in range(n):
+            if d == depth:
+                vals[base + j] = cv[j]
+            elif refine[d][j]:
+                off[base + j] = child
+                child += 8
+            else:
+                vals[base + j] = 1000.0
+        base += n
+    rec = np.zeros((total, 36), np.uint8)
+    rec[:, :32] = vals.view(np.uint8).reshape(total, 32)
+    rec[:, 32:] = off.view(np.uint8).reshape(total, 4)
+    return rec.ravel()
+
+
+def subdivide(vpos4, idx, levels: int):
+    """Midpoint subdivision: per triangle (a,b,c) with edge midpoints ab, bc, ca
+    (created in that order on first use, value (u+v)*0.5 on all 4 components)
+    -> (a,ab,ca), (ab,b,bc), (ca,bc,c), (ab,bc,ca)."""
+    V = [tuple(r) for r in np.asarray(vpos4, np.float32)]
+    I = np.asarray(idx, np.uint32).tolist()
+    half = np.float32(0.5)
+    for _ in range(levels):
+        mid = {}
+        J = []
+
+        def m(a, b):
+            k = (a, b) if a < b else (b, a)
+            r = mid.get(k)
+            if r is None:
+                r = len(V)
+                V.append(tuple((np.float32(V[a][c]) + np.float32(V[b][c])) * half for c in range(4)))
+                mid[k] = r
+            return r
+        for t in range(len(I) // 3):
+            a, b, c = I[3 * t:3 * t + 3]
+            ab, bc, ca = m(a, b), m(b, c), m(c, a)
+            J += [a, ab, ca, ab, b, bc, ca, bc, c, ab, bc, ca]
+        I = J
+    return np.array(V, np.float32).reshape(-1, 4), np.array(I, np.uint32)

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/rtamd.h"
+#include "rt_error.h"
 #include "rt_host.h"
 #include "rt_layout.h"
 #include "rt_math.h"
@@ -21,19 +22,18 @@
 
 using namespace rtd;
 
-namespace {
-
+namespace rterr {
 thread_local std::string g_err;
-int set_err(int code, const std::string &msg) {
+int set(int code, const std::string &msg) {
   g_err = msg;
   return code;
 }
-#define HIP_TRY(expr)                                                                   \
-  do {                                                                                  \
-    hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess)                                                               \
-      return set_err(RT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
-  } while (0)
+const char *get() { return g_err.c_str(); }
+}  // namespace rterr
+
+namespace {
+
+inline int set_err(int code, const std::string &msg) { return rterr::set(code, msg); }
 
 constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
 constexpr int kTile = 16;
@@ -685,7 +685,7 @@ int upload(T **dst, const T *src, size_t n, int64_t &bytes) {
 
 extern "C" {
 
-const char *rt_last_error(void) { return g_err.c_str(); }
+const char *rt_last_error(void) { return rterr::get(); }
 int rt_abi_version(void) { return RTAMD_ABI_VERSION; }
 
 int rt_device_count(void) {

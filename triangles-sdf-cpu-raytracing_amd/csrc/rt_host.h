@@ -43,6 +43,32 @@ struct OctGpu {
 };
 bool flatten_octree(const uint8_t *nodes36, int64_t count, OctGpu &out, std::string &err);
 
+// ---- mesh -> SDF construction (rt_meshops.cpp) ----
+// Feature order of the closest-point regions (Ericson, RTCD 5.1.5):
+// 0..2 vertex a,b,c; 3 edge ab; 4 edge ac; 5 edge bc; 6 face.
+constexpr int kSdfFeatures = 7;
+struct SdfMeshHost {
+  BVHGpu bvh;               // the renderer's BVH8 over the same triangles
+  std::vector<float> tri;   // per GPU leaf-order triangle: a.xyz,id | b.xyz,0 | c.xyz,0
+  std::vector<float> pn;    // per ORIGINAL triangle: 7 x float4 angle-weighted pseudonormals
+};
+bool prep_sdf_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                   SdfMeshHost &out, std::string &err);
+
+// Loop-free midpoint subdivision, `levels` times (config-5 stand-in mesh).
+bool subdivide_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, int levels,
+                    Mesh &out, std::string &err);
+
+// Sparse SDF octree in the reference's 36-byte node format, built top-down:
+// a node at depth d < depth is refined when |sdf(centre)| <= half-diagonal;
+// unrefined nodes become empty leaves (values 1000), nodes at `depth` become
+// leaves holding the SDF at their 8 corners; inner nodes hold zeros. Nodes are
+// in BFS order with the 8 children of a node contiguous (id (x<<2)|(y<<1)|z).
+// `query(points xyz, n, out)` evaluates the SDF at n points.
+using SdfQuery = bool (*)(void *ctx, const float *p3, int64_t n, float *out, std::string &err);
+bool build_sdf_octree(SdfQuery query, void *ctx, int depth, std::vector<uint8_t> &nodes36,
+                      std::string &err);
+
 void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
                      float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]);
 

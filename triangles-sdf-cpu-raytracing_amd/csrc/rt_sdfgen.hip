@@ -1,0 +1,362 @@
+// rt_sdfgen.hip -- mesh -> signed distance construction on the GPU (SURVEY.md
+// 8(f) rank 1): the deterministic generator of the large grid / octree
+// stand-ins for BASELINE configs 3 and 4 (example_grid_large.grid and
+// example_octree_large.octree are not in the reference, .MISSING_LARGE_BLOBS).
+//
+// One thread per query point. A closest-point query walks the renderer's own
+// BVH8 (rt_layout.h GNode) nearest-box-first with a lane-interleaved LDS
+// stack of (box distance^2, child word), pruning boxes farther than the best
+// distance plus an absolute slack of 1e-5 (>> the f32 rounding of points in
+// [-1,1]^3), so the result equals the brute-force minimum over all triangles
+// bit for bit, ties included (lexicographic (d^2, triangle id)). The closest
+// point and its region follow Ericson (RTCD 5.1.5) op for op; the sign comes
+// from the host-computed pseudonormal of the closest feature (rt_meshops.cpp).
+// Lattice queries map a 4x4x4 brick of samples to each 64-lane wave.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtamd.h"
+#include "rt_error.h"
+#include "rt_host.h"
+#include "rt_layout.h"
+#include "rt_math.h"
+
+using namespace rtd;
+
+struct rt_sdf_mesh {
+  rth::SdfMeshHost host;
+  rtl::GNode *d_nodes = nullptr;
+  float4 *d_tri = nullptr;
+  float4 *d_pn = nullptr;
+  uint32_t root = rtl::kInvalidChild;
+  int32_t stack_cap = 0;
+  int device = 0;
+  int32_t oct_depth = -1;          // octree cache (two-call protocol of rt_sdf_mesh_octree)
+  std::vector<uint8_t> oct_nodes;
+};
+
+namespace {
+
+constexpr int kWave = 64;
+
+struct SdfDev {
+  const rtl::GNode *nodes;
+  const float4 *tri;
+  const float4 *pn;
+  uint32_t root;
+};
+
+// Ericson, Real-Time Collision Detection 5.1.5 ClosestPtPointTriangle, with
+// the Voronoi region reported: 0..2 vertex a,b,c; 3 ab; 4 ac; 5 bc; 6 face.
+__device__ __forceinline__ f3 closest_on_tri(f3 p, f3 a, f3 b, f3 c, int &feat) {
+  const f3 ab = b - a, ac = c - a, ap = p - a;
+  const float d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.0f && d2 <= 0.0f) { feat = 0; return a; }
+  const f3 bp = p - b;
+  const float d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.0f && d4 <= d3) { feat = 1; return b; }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0f && d1 >= 0.0f && d3 <= 0.0f) {
+    const float v = d1 / (d1 - d3);
+    feat = 3;
+    return a + ab * v;
+  }
+  const f3 cp = p - c;
+  const float d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0.0f && d5 <= d6) { feat = 2; return c; }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) {
+    const float w = d2 / (d2 - d6);
+    feat = 4;
+    return a + ac * w;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.0f && (d4 - d3) >= 0.0f && (d5 - d6) >= 0.0f) {
+    const float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    feat = 5;
+    return b + (c - b) * w;
+  }
+  const float denom = 1.0f / (va + vb + vc);
+  const float v = vb * denom, w = vc * denom;
+  feat = 6;
+  return a + ab * v + ac * w;
+}
+
+__device__ __forceinline__ float box_d2(const float *bx, f3 p) {
+  const float dx = fmaxf(fmaxf(bx[0] - p.x, p.x - bx[3]), 0.0f);
+  const float dy = fmaxf(fmaxf(bx[1] - p.y, p.y - bx[4]), 0.0f);
+  const float dz = fmaxf(fmaxf(bx[2] - p.z, p.z - bx[5]), 0.0f);
+  return dx * dx + dy * dy + dz * dz;
+}
+
+__device__ __forceinline__ float prune_bound(float best) {
+  if (!(best < kInf)) return kInf;
+  const float r = __builtin_sqrtf(best) + 1e-5f;
+  return r * r;
+}
+
+// Signed distance at p. st_d / st_w: this lane's LDS stack columns (stride 64).
+__device__ float sdf_query(const SdfDev &m, f3 p, float *st_d, uint32_t *st_w) {
+  float best = kInf, bound = kInf;
+  uint32_t best_id = 0xFFFFFFFFu;
+  int best_feat = 0;
+  f3 best_q{0.0f, 0.0f, 0.0f};
+  int sp = 0;
+  uint32_t word = m.root;
+  while (true) {
+    if (word != rtl::kInvalidChild) {
+      if (word & rtl::kLeafBit) {
+        const uint32_t first = (word >> 3) & rtl::kMaxLeafFirstTri, n = (word & 7u) + 1u;
+        for (uint32_t k = 0; k < n; ++k) {
+          const float4 A = m.tri[3 * (first + k)], B = m.tri[3 * (first + k) + 1], C = m.tri[3 * (first + k) + 2];
+          int feat;
+          const f3 q = closest_on_tri(p, f3{A.x, A.y, A.z}, f3{B.x, B.y, B.z}, f3{C.x, C.y, C.z}, feat);
+          const f3 e = p - q;
+          const float d2 = dot(e, e);
+          const uint32_t id = __float_as_uint(A.w);
+          if (d2 < best || (d2 == best && id < best_id)) {
+            best = d2;
+            best_id = id;
+            best_feat = feat;
+            best_q = q;
+            bound = prune_bound(best);
+          }
+        }
+      } else {
+        const rtl::GNode &nd = m.nodes[word];
+        float bx[48];
+        const float4 *b4 = reinterpret_cast<const float4 *>(nd.box);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          const float4 v = b4[i];
+          bx[4 * i] = v.x; bx[4 * i + 1] = v.y; bx[4 * i + 2] = v.z; bx[4 * i + 3] = v.w;
+        }
+        const uint4 c0 = reinterpret_cast<const uint4 *>(nd.child)[0];
+        const uint4 c1 = reinterpret_cast<const uint4 *>(nd.child)[1];
+        float t[8];
+        uint32_t id[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) t[c] = id[c] == rtl::kInvalidChild ? kInf : box_d2(bx + 6 * c, p);
+        sort8(t, id);
+        // push farthest first so the nearest is popped next
+#pragma unroll
+        for (int c = 7; c >= 0; --c) {
+          if (id[c] != rtl::kInvalidChild && t[c] <= bound) {
+            st_d[sp * kWave] = t[c];
+            st_w[sp * kWave] = id[c];
+            ++sp;
+          }
+        }
+      }
+    }
+    // pop the next box that can still hold a closer triangle
+    word = rtl::kInvalidChild;
+    while (sp > 0) {
+      --sp;
+      if (st_d[sp * kWave] <= bound) {
+        word = st_w[sp * kWave];
+        break;
+      }
+    }
+    if (word == rtl::kInvalidChild) break;
+  }
+  if (best_id == 0xFFFFFFFFu) return kInf;
+  const float4 N = m.pn[7u * best_id + (uint32_t)best_feat];
+  const f3 e = p - best_q;
+  const float s = e.x * N.x + e.y * N.y + e.z * N.z;
+  const float d = __builtin_sqrtf(best);
+  return s < 0.0f ? -d : d;
+}
+
+// LATTICE: sample (i,j,k) of an n0 x n1 x n2 lattice over [-1,1]^3,
+// p = 2*i/(n-1) - 1 per axis (the inverse of SDFGrid::sdf's
+// q = (p+1)/2*(size-1), grid_raytracing.cpp:7-62), out[(i*n1+j)*n2+k].
+// Dynamic LDS: cap x 64 floats (box distances) then cap x 64 child words.
+template <bool LATTICE>
+__global__ __launch_bounds__(kWave) void sdf_kernel(SdfDev m, const float *p3, int64_t n, uint32_t n0,
+                                                   uint32_t n1, uint32_t n2, int cap, float *out) {
+  extern __shared__ uint32_t lds[];
+  float *st_d = reinterpret_cast<float *>(lds) + threadIdx.x;
+  uint32_t *st_w = lds + (size_t)cap * kWave + threadIdx.x;
+  f3 p;
+  int64_t o;
+  if (LATTICE) {
+    const uint32_t by = (n1 + 3) / 4, bz = (n2 + 3) / 4;
+    const uint64_t b = blockIdx.x;
+    const uint32_t ib = (uint32_t)(b / ((uint64_t)by * bz));
+    const uint32_t rem = (uint32_t)(b % ((uint64_t)by * bz));
+    const uint32_t jb = rem / bz, kb = rem % bz;
+    const uint32_t i = ib * 4 + (threadIdx.x >> 4), j = jb * 4 + ((threadIdx.x >> 2) & 3),
+                   k = kb * 4 + (threadIdx.x & 3);
+    if (i >= n0 || j >= n1 || k >= n2) return;
+    p = f3{2.0f * (float)i / (float)(n0 - 1) - 1.0f, 2.0f * (float)j / (float)(n1 - 1) - 1.0f,
+           2.0f * (float)k / (float)(n2 - 1) - 1.0f};
+    o = ((int64_t)i * n1 + j) * n2 + k;
+  } else {
+    o = (int64_t)blockIdx.x * kWave + threadIdx.x;
+    if (o >= n) return;
+    p = f3{p3[3 * o], p3[3 * o + 1], p3[3 * o + 2]};
+  }
+  out[o] = sdf_query(m, p, st_d, st_w);
+}
+
+template <class T>
+int upload(T **d, const T *h, size_t n) {
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(d), std::max<size_t>(n, 1) * sizeof(T)));
+  if (n) HIP_TRY(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+SdfDev dev_of(const rt_sdf_mesh *m) { return SdfDev{m->d_nodes, m->d_tri, m->d_pn, m->root}; }
+
+size_t lds_bytes(const rt_sdf_mesh *m) { return (size_t)m->stack_cap * kWave * 8; }
+
+// Evaluate n points (device buffers) on the null stream and wait.
+int query_device(rt_sdf_mesh *m, const float *d_p3, int64_t n, float *d_out) {
+  if (n <= 0) return RT_OK;
+  const int64_t blocks = (n + kWave - 1) / kWave;
+  if (blocks > 0x7FFFFFFF) return rterr::set(RT_E_INVALID, "too many points");
+  hipLaunchKernelGGL(sdf_kernel<false>, dim3((uint32_t)blocks), dim3(kWave), lds_bytes(m), 0, dev_of(m), d_p3,
+                     n, 0u, 0u, 0u, m->stack_cap, d_out);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  return RT_OK;
+}
+
+int query_host(rt_sdf_mesh *m, const float *p3, int64_t n, float *out) {
+  if (n <= 0) return RT_OK;
+  HIP_TRY(hipSetDevice(m->device));
+  float *dp = nullptr, *dd = nullptr;
+  int rc = RT_OK;
+  if (hipMalloc(&dp, (size_t)n * 12) != hipSuccess || hipMalloc(&dd, (size_t)n * 4) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, "hipMalloc failed for the query points");
+  } else if (hipMemcpy(dp, p3, (size_t)n * 12, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, "hipMemcpy H2D failed");
+  } else if ((rc = query_device(m, dp, n, dd)) == RT_OK &&
+             hipMemcpy(out, dd, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, "hipMemcpy D2H failed");
+  }
+  if (dp) (void)hipFree(dp);
+  if (dd) (void)hipFree(dd);
+  return rc;
+}
+
+bool octree_query(void *ctx, const float *p3, int64_t n, float *out, std::string &err) {
+  if (query_host(static_cast<rt_sdf_mesh *>(ctx), p3, n, out) != RT_OK) {
+    err = rterr::get();
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_sdf_mesh_create(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                       rt_sdf_mesh **out) {
+  if (!out || (!vpos4 && nverts) || (!idx && nidx) || nverts < 0 || nidx < 0)
+    return rterr::set(RT_E_INVALID, "bad mesh arguments");
+  *out = nullptr;
+  rt_sdf_mesh *m = new rt_sdf_mesh();
+  std::string err;
+  if (!rth::prep_sdf_mesh(vpos4, nverts, idx, nidx, m->host, err)) {
+    delete m;
+    return rterr::set(RT_E_INVALID, err);
+  }
+  const rth::BVHGpu &b = m->host.bvh;
+  m->root = b.root_word;
+  m->stack_cap = 7 * std::max(b.max_depth, 1) + 1;
+  if ((size_t)m->stack_cap * kWave * 8 > 160 * 1024) {
+    delete m;
+    return rterr::set(RT_E_INVALID, "BVH too deep for the SDF query stack");
+  }
+  int rc = hipGetDevice(&m->device) == hipSuccess ? RT_OK : rterr::set(RT_E_DEVICE, "no HIP device");
+  if (rc == RT_OK) rc = upload(&m->d_nodes, b.nodes.data(), b.nodes.size());
+  if (rc == RT_OK) rc = upload(&m->d_tri, reinterpret_cast<const float4 *>(m->host.tri.data()), m->host.tri.size() / 4);
+  if (rc == RT_OK) rc = upload(&m->d_pn, reinterpret_cast<const float4 *>(m->host.pn.data()), m->host.pn.size() / 4);
+  if (rc != RT_OK) {
+    rt_sdf_mesh_destroy(m);
+    return rc;
+  }
+  *out = m;
+  return RT_OK;
+}
+
+int rt_sdf_mesh_points(rt_sdf_mesh *m, const float *p3, int64_t n, float *dist) {
+  if (!m || n < 0 || (n && (!p3 || !dist))) return rterr::set(RT_E_INVALID, "bad arguments");
+  return query_host(m, p3, n, dist);
+}
+
+int rt_sdf_mesh_grid(rt_sdf_mesh *m, const uint32_t size[3], float *values) {
+  if (!m || !size || !values) return rterr::set(RT_E_INVALID, "bad arguments");
+  for (int a = 0; a < 3; ++a)
+    if (size[a] < 2 || size[a] > 4096) return rterr::set(RT_E_INVALID, "grid size must be in [2, 4096]");
+  const int64_t n = (int64_t)size[0] * size[1] * size[2];
+  const uint64_t blocks = (uint64_t)((size[0] + 3) / 4) * ((size[1] + 3) / 4) * ((size[2] + 3) / 4);
+  if (blocks > 0x7FFFFFFFull) return rterr::set(RT_E_INVALID, "grid too large");
+  HIP_TRY(hipSetDevice(m->device));
+  float *d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)n * 4));
+  hipLaunchKernelGGL(sdf_kernel<true>, dim3((uint32_t)blocks), dim3(kWave), lds_bytes(m), 0, dev_of(m), nullptr,
+                     n, size[0], size[1], size[2], m->stack_cap, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(values, d, (size_t)n * 4, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return rterr::set(RT_E_DEVICE, std::string("sdf grid: ") + hipGetErrorString(e));
+  return RT_OK;
+}
+
+int rt_sdf_mesh_octree(rt_sdf_mesh *m, int32_t depth, int64_t *count, void *nodes36) {
+  if (!m || !count) return rterr::set(RT_E_INVALID, "bad arguments");
+  if (m->oct_depth != depth) {
+    std::string err;
+    std::vector<uint8_t> nodes;
+    if (!rth::build_sdf_octree(octree_query, m, depth, nodes, err))
+      return rterr::set(err.rfind("octree", 0) == 0 ? RT_E_INVALID : RT_E_DEVICE, err);
+    m->oct_nodes.swap(nodes);
+    m->oct_depth = depth;
+  }
+  const int64_t n = (int64_t)(m->oct_nodes.size() / 36);
+  if (nodes36) {
+    if (*count < n) return rterr::set(RT_E_INVALID, "node buffer too small");
+    std::memcpy(nodes36, m->oct_nodes.data(), m->oct_nodes.size());
+  }
+  *count = n;
+  return RT_OK;
+}
+
+int rt_sdf_mesh_destroy(rt_sdf_mesh *m) {
+  if (!m) return RT_OK;
+  if (m->d_nodes) (void)hipFree(m->d_nodes);
+  if (m->d_tri) (void)hipFree(m->d_tri);
+  if (m->d_pn) (void)hipFree(m->d_pn);
+  delete m;
+  return RT_OK;
+}
+
+int rt_mesh_subdivide(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, int32_t levels,
+                      float *out_vpos4, int64_t *out_nverts, uint32_t *out_idx, int64_t *out_nidx) {
+  if ((!vpos4 && nverts) || (!idx && nidx) || nverts < 0 || !out_nverts || !out_nidx)
+    return rterr::set(RT_E_INVALID, "bad arguments");
+  rth::Mesh r;
+  std::string err;
+  if (!rth::subdivide_mesh(vpos4, nverts, idx, nidx, levels, r, err)) return rterr::set(RT_E_INVALID, err);
+  const int64_t nv = (int64_t)(r.vpos4.size() / 4), ni = (int64_t)r.idx.size();
+  if (out_vpos4 || out_idx) {
+    if (!out_vpos4 || !out_idx || *out_nverts < nv || *out_nidx < ni)
+      return rterr::set(RT_E_INVALID, "output buffers too small");
+    std::memcpy(out_vpos4, r.vpos4.data(), r.vpos4.size() * 4);
+    std::memcpy(out_idx, r.idx.data(), r.idx.size() * 4);
+  }
+  *out_nverts = nv;
+  *out_nidx = ni;
+  return RT_OK;
+}
+
+}  // extern "C"

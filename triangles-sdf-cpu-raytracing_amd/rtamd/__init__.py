@@ -6,14 +6,15 @@ package only marshals arguments.
 """
 from ._lib import EXPORTED, LIB_PATH, RT_FLAG_CLEAR, RenderParams, RtError, Tile, build, lib
 from .api import (BVHBuilder, Camera, FrameBuffer, HitInfo, IScene, Plane, Renderer, SceneUnion,
-                  SDFGrid, SDFOctree, ShadingMode, SimpleMesh, camera_matrices, device_count,
-                  load_mesh_from_obj, load_sdf_grid, load_sdf_octree, render_params)
+                  SDFGrid, SDFMesh, SDFOctree, ShadingMode, SimpleMesh, camera_matrices, device_count,
+                  load_mesh_from_obj, load_sdf_grid, load_sdf_octree, render_params, subdivide_mesh)
 from . import data, tiles, workloads
 
 __all__ = [
     "EXPORTED", "LIB_PATH", "RT_FLAG_CLEAR", "RenderParams", "RtError", "Tile", "build", "lib",
     "BVHBuilder", "Camera", "FrameBuffer", "HitInfo", "IScene", "Plane", "Renderer", "SceneUnion",
-    "SDFGrid", "SDFOctree", "ShadingMode", "SimpleMesh", "camera_matrices", "device_count",
-    "load_mesh_from_obj", "load_sdf_grid", "load_sdf_octree", "render_params", "data",
+    "SDFGrid", "SDFMesh", "SDFOctree", "ShadingMode", "SimpleMesh", "camera_matrices", "device_count",
+    "load_mesh_from_obj", "load_sdf_grid", "load_sdf_octree", "render_params", "subdivide_mesh",
+    "data",
     "tiles", "workloads",
 ]

@@ -81,6 +81,14 @@ _SIGS = {
                                 C.c_uint32, C.c_void_p, C.c_void_p]),
     "rt_bench_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "rt_sdf_mesh_create": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                     C.POINTER(C.c_void_p)]),
+    "rt_sdf_mesh_points": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "rt_sdf_mesh_grid": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_sdf_mesh_octree": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.c_void_p]),
+    "rt_sdf_mesh_destroy": (C.c_int, [C.c_void_p]),
+    "rt_mesh_subdivide": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p,
+                                    C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

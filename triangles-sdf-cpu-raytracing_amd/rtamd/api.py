@@ -29,7 +29,7 @@ __all__ = [
     "ShadingMode", "SimpleMesh", "FrameBuffer", "Camera", "Renderer", "HitInfo", "IScene",
     "BVHBuilder", "SDFGrid", "SDFOctree", "Plane", "SceneUnion", "load_mesh_from_obj",
     "load_sdf_grid", "load_sdf_octree", "camera_matrices", "render_params", "RtError",
-    "RT_FLAG_CLEAR", "Tile", "device_count",
+    "RT_FLAG_CLEAR", "Tile", "device_count", "SDFMesh", "subdivide_mesh",
 ]
 
 
@@ -340,3 +340,65 @@ class Renderer:
         P = render_params(camera.position(), camera.view_inv(), proj_inv, self.lightPos,
                           self.shadingMode, self.enableShadows, self.enableReflections)
         return base.render(P, frame_buffer.color, frame_buffer.t, clear=False)
+
+
+# --------------------------------------------- mesh -> SDF --
+class SDFMesh:
+    """A triangle mesh prepared on the GPU for signed-distance queries
+    (rt_sdf_mesh_*): point queries, SDFGrid lattices and sparse SDFOctrees in
+    the reference's file formats (grid_raytracing.cpp:127-134,
+    octree_raytracing.cpp:8-16). Generates the config-3/4 stand-ins."""
+
+    def __init__(self, mesh: SimpleMesh):
+        v = np.ascontiguousarray(mesh.vPos4f, np.float32)
+        i = np.ascontiguousarray(mesh.indices, np.uint32)
+        h = C.c_void_p()
+        check(lib().rt_sdf_mesh_create(_p(v), len(v), _p(i), len(i), C.byref(h)))
+        self._h = h
+
+    def points(self, p3) -> np.ndarray:
+        p3 = np.ascontiguousarray(p3, np.float32).reshape(-1, 3)
+        out = np.empty(len(p3), np.float32)
+        check(lib().rt_sdf_mesh_points(self._h, _p(p3), len(p3), _p(out)))
+        return out
+
+    def grid(self, size):
+        """-> (size uint32[3], values float32[sx*sy*sz]) as SDFGrid holds them."""
+        size = np.ascontiguousarray(np.broadcast_to(np.asarray(size, np.uint32), (3,)))
+        vals = np.empty(int(size[0]) * int(size[1]) * int(size[2]), np.float32)
+        check(lib().rt_sdf_mesh_grid(self._h, _p(size), _p(vals)))
+        return size, vals
+
+    def octree(self, depth: int) -> np.ndarray:
+        """-> raw nodes, uint8 [count*36] (SDFOctreeNode records, BFS)."""
+        n = C.c_int64(0)
+        check(lib().rt_sdf_mesh_octree(self._h, int(depth), C.byref(n), None))
+        buf = np.empty(n.value * 36, np.uint8)
+        check(lib().rt_sdf_mesh_octree(self._h, int(depth), C.byref(n), _p(buf)))
+        return buf
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_sdf_mesh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def subdivide_mesh(mesh: SimpleMesh, levels: int) -> SimpleMesh:
+    """Midpoint subdivision (rt_mesh_subdivide): the config-5 stand-in mesh."""
+    L = lib()
+    v = np.ascontiguousarray(mesh.vPos4f, np.float32)
+    i = np.ascontiguousarray(mesh.indices, np.uint32)
+    nv, ni = C.c_int64(0), C.c_int64(0)
+    check(L.rt_mesh_subdivide(_p(v), len(v), _p(i), len(i), int(levels), None, C.byref(nv), None,
+                              C.byref(ni)))
+    ov = np.empty((nv.value, 4), np.float32)
+    oi = np.empty(ni.value, np.uint32)
+    check(L.rt_mesh_subdivide(_p(v), len(v), _p(i), len(i), int(levels), _p(ov), C.byref(nv), _p(oi),
+                              C.byref(ni)))
+    return SimpleMesh(ov, oi)
