@@ -5,9 +5,14 @@ Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355
 Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
 1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
 the pure intersection hot path), over a deterministic 64-frame camera orbit
-(SURVEY.md 8(d)). A "step" is one frame. The SDF grid (configs[2] shape, on the
-shipped 65^3 example_grid.grid) is measured the same way and reported under
-"extra" at N=1.
+(SURVEY.md 8(d)). A "step" is one frame. At N=1 the other BASELINE configs
+are measured the same way and reported under "extra" (rank 0): the SDF grid
+(configs[2]) on a 256^3 SDF of stanford-bunny generated on the GPU (stand-in:
+example_grid_large.grid is missing from the reference) and on the shipped
+65^3 example_grid.grid; the octree (configs[3]) at 3840x2160 on a depth-8
+generated octree (stand-in for example_octree_large.octree) and on the
+shipped sdf_6.octree; and the config-5 mesh stand-in (stanford-bunny
+subdivided twice, 1,111,216 triangles) at 3840x2160.
 
 Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every frame is
 split into 16-row bands dealt round-robin to the ranks (load balance: the model
@@ -59,6 +64,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
 
 
@@ -76,21 +84,24 @@ def frame_params(n_frames):
             for k in range(n_frames)]
 
 
-def run_single(scene, params, warmup, steps):
-    """N=1: full frames, render kernel only. Returns (wall_s, kernel_ms_avg)."""
+def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG):
+    """N=1: full frames, render kernel only, launched on torch's current stream
+    (the events below are recorded on that same stream). Returns (wall_s,
+    kernel_ms_avg, buffers)."""
     dev = torch.device("cuda")
-    color = torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev)
-    tbuf = torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev)
+    color = torch.empty((H, W), dtype=torch.int32, device=dev)
+    tbuf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
     for k in range(warmup):
-        scene.render_device(params[k], color.data_ptr(), tbuf.data_ptr(), W_IMG, H_IMG, clear=True)
+        scene.render_device(params[k], color.data_ptr(), tbuf.data_ptr(), W, H, clear=True, stream=stream)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
         evs[k][0].record()
-        scene.render_device(params[warmup + k], color.data_ptr(), tbuf.data_ptr(), W_IMG, H_IMG,
-                            clear=True)
+        scene.render_device(params[warmup + k], color.data_ptr(), tbuf.data_ptr(), W, H, clear=True,
+                            stream=stream)
         evs[k][1].record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -99,8 +110,12 @@ def run_single(scene, params, warmup, steps):
 
 
 def run_distributed(scene, params, warmup, steps, rank, world, band):
-    """N>1: row bands per rank + one RCCL gather per frame to rank 0."""
+    """N>1: row bands per rank + one RCCL gather per frame to rank 0.
+    With the gloo backend (RTAMD_DIST_BACKEND=gloo: several ranks sharing one
+    GPU, for testing the protocol on a 1-GPU box) the packed bands are staged
+    through host memory and gathered synchronously."""
     dev = torch.device("cuda", torch.cuda.current_device())
+    staged = dist.get_backend() == "gloo"
     tiles = [rtamd.Tile(band, r, world, 0) for r in range(world)]
     per = max(rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(t)) for t in tiles)
     # packed slot: [colour (per) | t (per)] as int32 words, double-buffered; rank 0
@@ -120,9 +135,10 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
         rtamd._lib.check(rtamd.lib().rt_untile_device(
             ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * per), 2 * per,
             ctypes.c_void_p(frame_c.data_ptr()), ctypes.c_void_p(frame_t.data_ptr()), W_IMG, H_IMG,
-            ctypes.byref(tiles[0]), None))
+            ctypes.byref(tiles[0]), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
 
     def step(k, timed):
+        last[0] = k
         slot = k & 1
         b = bufs[slot]
         if pending[slot] is not None:
@@ -134,15 +150,24 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         scene.render_device(params[k], b.data_ptr(), b.data_ptr() + 4 * per, W_IMG, H_IMG,
-                            clear=True, tile=tile)
+                            clear=True, tile=tile, stream=torch.cuda.current_stream().cuda_stream)
         if timed:
             e1.record()
             ev.append((e0, e1))
+        if staged:
+            host = b.cpu()
+            lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+            dist.gather(host, gather_list=lst, dst=0)
+            if rank == 0:
+                stacked[slot].copy_(torch.stack(lst))
+                untile(slot)
+            return
         pending[slot] = dist.gather(b, gather_list=recv[slot] if rank == 0 else None, dst=0,
                                     async_op=True)
 
     def drain():
-        for slot in (0, 1):
+        # oldest first, so the frame left in frame_c/frame_t is the last one rendered
+        for slot in (last[0] + 1) & 1, last[0] & 1:
             if pending[slot] is not None:
                 pending[slot].wait()
                 if rank == 0:
@@ -150,6 +175,7 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
                 pending[slot] = None
 
     pending = [None, None]
+    last = [0]
     for k in range(warmup):
         step(k, False)
     drain()
@@ -164,13 +190,12 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
     dist.barrier()
     wall = time.perf_counter() - t0
     kms = sum(a.elapsed_time(b) for a, b in ev) / steps
-    return wall, kms, tile
+    return wall, kms, tile, (frame_c, frame_t)
 
 
-def roofline(scene, params, tile, kms):
-    c = scene.count_work(params, W_IMG, H_IMG, clear=True, tile=tile)
-    npx = (rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(tile))
-           if tile is not None else W_IMG * H_IMG)
+def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG):
+    c = scene.count_work(params, W, H, clear=True, tile=tile)
+    npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
     algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params)
     achieved = algo / (kms * 1e-3) / 1e9
     per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
@@ -178,6 +203,102 @@ def roofline(scene, params, tile, kms):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
             "work_per_ray": per_ray}
+
+
+def pmc_traffic(workload, W, H, frames=16):
+    """HBM bytes per launch of the headline render kernel from rocprofv3 PMC
+    counters, collected in two separate --pmc passes (FETCH_SIZE, WRITE_SIZE
+    cannot share a pass) over tools/prof_frames.py, as MI355X_MICROARCH.md's
+    HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+    FETCH_SIZE reports half the bytes of coalesced reads, so it is doubled.
+    Runs as child processes BEFORE this process touches the GPU. Returns
+    (bytes_per_launch | None, detail dict)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, {"error": "rocprofv3 not found"}
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="rtamd_pmc_", dir="/tmp")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-k", "10", "180", prof, "--pmc", ctr, "--output-format", "csv", "-d", d,
+                   "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_frames.py"),
+                   "--workload", workload, "--frames", str(frames), "--W", str(W), "--H", str(H)]
+            r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
+            if r.returncode != 0:
+                return None, {"error": f"{ctr} pass rc={r.returncode}: {r.stderr[-300:]}"}
+            per = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if "render_kernel" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                            per.append(float(row["Counter_Value"]))
+            if not per:
+                return None, {"error": f"no {ctr} rows for render_kernel"}
+            vals[ctr] = sum(per) / len(per)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return fetch + write, {"fetch_bytes": round(fetch), "write_bytes": round(write),
+                           "raw_kib": {k: round(v, 1) for k, v in vals.items()},
+                           "launches": frames, "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
+
+
+def standin_scenes(which):
+    """BASELINE configs 3-5 stand-ins, generated deterministically on the GPU
+    from the shipped stanford-bunny.obj (rt_sdf_mesh_* / rt_mesh_subdivide)."""
+    from rtamd import data
+    bunny = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
+    if which == "mesh_large":
+        return rtamd.BVHBuilder(rtamd.subdivide_mesh(bunny, 2))
+    sm = rtamd.SDFMesh(bunny)
+    if which == "grid":
+        return rtamd.SDFGrid(*sm.grid(256))
+    return rtamd.SDFOctree(sm.octree(8))
+
+
+EXTRAS = [
+    # key, scene source, W, H, description
+    ("grid", "grid", 1920, 1080,
+     "stanford-bunny SDF 256^3 grid generated on the GPU (stand-in for the missing "
+     "example_grid_large.grid, BASELINE configs[2])"),
+    ("grid_shipped", "example_grid.grid", 1920, 1080, "shipped example_grid.grid (65^3)"),
+    ("octree", "octree", 3840, 2160,
+     "stanford-bunny SDF octree of depth 8 generated on the GPU (stand-in for the missing "
+     "example_octree_large.octree, BASELINE configs[3])"),
+    ("octree_shipped", "sdf_6.octree", 3840, 2160, "shipped sdf_6.octree"),
+    ("mesh_large", "mesh_large", 3840, 2160,
+     "stanford-bunny midpoint-subdivided twice, 1,111,216 triangles (stand-in for the missing "
+     "MotorcycleCylinderHead.obj, BASELINE configs[4]), 1 GPU"),
+]
+
+
+def run_extras(warmup, steps):
+    out = {}
+    for key, src, W, H, desc in EXTRAS:
+        if "." in src:
+            kind, payload, _ = WL.load_input(src)
+            sc = WL.make_scene(kind, payload)
+        else:
+            sc = standin_scenes(src)
+        sc.set_plane(None)
+        orbit = WL.orbit_positions(64)
+        prm = [WL.params_for(orbit[k % 64], W, H, rtamd.ShadingMode.Normal) for k in range(warmup + steps)]
+        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H)
+        out[key] = {"workload": f"{desc}, {W}x{H} primary rays, same orbit",
+                    "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
+                    "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
+                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H)}
+        sc.close()
+        torch.cuda.synchronize()
+    return out
 
 
 def cpu_baseline(name, budget_s):
@@ -219,27 +340,51 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    if world > 1:
+    use_dist = world > 1 or a.dist
+    pmc = None
+    if not use_dist and not a.no_pmc:
+        pmc = pmc_traffic(a.workload, W_IMG, H_IMG)  # child processes, before this one inits the GPU
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
+    device = local % ndev  # ranks > devices only for the gloo protocol test
+    torch.cuda.set_device(device)
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    rtamd.lib().rt_set_device(local)
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        backend = os.environ.get("RTAMD_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    rtamd._lib.check(rtamd.lib().rt_set_device(device))
 
     kind, payload, _ = WL.load_input(a.workload)
     scene = WL.make_scene(kind, payload)
     scene.set_plane(None)
     params = frame_params(a.warmup + a.steps)
 
-    if world == 1:
+    if not use_dist:
         wall, kms, _ = run_single(scene, params, a.warmup, a.steps)
         tile = None
     else:
-        wall, kms, tile = run_distributed(scene, params, a.warmup, a.steps, rank, world, a.band_rows)
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        wall, kms, tile, frame = run_distributed(scene, params, a.warmup, a.steps, rank, world,
+                                                 a.band_rows)
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
+        if rank == 0:  # the gathered last frame must equal a whole-frame render of it
+            _, _, (c1, t1) = run_single(scene, params[-1:], 0, 1)
+            check_equal = bool(torch.equal(c1, frame[0]) and torch.equal(t1.view(torch.int32),
+                                                                         frame[1].view(torch.int32)))
 
     rl = roofline(scene, params[a.warmup:], tile, kms)
+    if pmc is not None:
+        rl["traffic"] = None if pmc[0] is None else round(pmc[0])
+        rl["traffic_detail"] = pmc[1]
     total_rays = W_IMG * H_IMG * a.steps
     value = total_rays / wall / 1e6
     out = {
@@ -251,25 +396,19 @@ def main():
                                "(BASELINE configs[1]); Normal shading, no plane",
                    "resolution": [W_IMG, H_IMG], "camera": "orbit r=2.5 h=0.5 fovy 45",
                    "parallelism": f"row bands of {a.band_rows} rows x {world} GPUs + RCCL gather"
-                   if world > 1 else "1 GPU, 1 thread per pixel"},
+                   if use_dist else "1 GPU, 1 thread per pixel"},
         "roofline": rl,
     }
-    if rank == 0 and world == 1 and not a.no_extra:
-        gkind, gpayload, _ = WL.load_input("example_grid.grid")
-        g = WL.make_scene(gkind, gpayload)
-        g.set_plane(None)
-        gwall, gkms, _ = run_single(g, params, a.warmup, a.steps)
-        out["extra"] = {"grid": {
-            "workload": "example_grid.grid (65^3, shipped stand-in for example_grid_large) "
-                        f"{W_IMG}x{H_IMG} primary rays",
-            "value": round(total_rays / gwall / 1e6, 1), "unit": "Mrays/s",
-            "ms_per_step": round(gwall * 1e3 / a.steps, 4),
-            "roofline": roofline(g, params[a.warmup:], None, gkms)}}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if use_dist and rank == 0:
+        out["frame_check"] = {"gathered_equals_single_render": check_equal,
+                              "backend": dist.get_backend()}
+    if rank == 0 and not use_dist and not a.no_extra:
+        out["extra"] = run_extras(min(a.warmup, 8), min(a.steps, 64))
+    if rank == 0 and not use_dist and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 
