@@ -43,9 +43,14 @@ print(f"  waves > 10us: {long.sum()}  ({long.mean()*100:.1f}%), their mean {dur[
 mxu = (buf[:, 2] & 0xFFFFFFFF).astype(np.int64)
 smu = (buf[:, 2] >> np.uint64(32)).astype(np.int64)
 order = np.argsort(dur)[::-1][:8]
-print("  slowest waves: dur_us max_lane_units sum_units ns_per_maxunit")
+print("  slowest waves: dur_us start_us end_us max_lane_units sum_units ns_per_maxunit")
 for i in order:
-    print(f"    {dur[i]/1e3:8.1f} {mxu[i]:6d} {smu[i]:8d} {dur[i]/max(mxu[i],1):8.0f}")
+    print(f"    {dur[i]/1e3:8.1f} {st[i]/1e3:8.1f} {en[i]/1e3:8.1f} {mxu[i]:6d} {smu[i]:8d} {dur[i]/max(mxu[i],1):8.0f}")
+# waves ending in the last 30% of the span: when did they start?
+late = en > 0.7 * en.max()
+print(f"  waves ending in the last 30% of the span: {late.sum()}, start p10/p50/p90 "
+      f"{np.percentile(st[late], 10)/1e3:.1f}/{np.percentile(st[late], 50)/1e3:.1f}/"
+      f"{np.percentile(st[late], 90)/1e3:.1f} us, duration p50 {np.percentile(dur[late], 50)/1e3:.1f} us")
 print(f"  SIMD efficiency (sum / 64*max over waves): {smu.sum() / max(64*mxu.sum(),1):.3f}")
 xcc = buf[:, 3] & 0xF
 for x in range(8):

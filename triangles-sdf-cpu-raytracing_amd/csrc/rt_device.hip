@@ -45,6 +45,8 @@ struct FrameArgs {
   int32_t W, H;
   uint32_t flags;
   int32_t band_rows, rank, nranks, rows_local;
+  const uint32_t *order;  // block -> tile schedule (NULL: blockIdx order)
+  uint32_t *cost;         // per-tile cost of this frame (shader cycles, max over waves), or NULL
 };
 
 // ---------------------------------------------------------- scene adapters --
@@ -263,8 +265,15 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
   unsigned long long t_start = 0;
   if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-  const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  uint32_t bx = blockIdx.x, by = blockIdx.y;
+  if (DIAG == 0 && fa.order) {  // cost-ordered schedule: this block renders tile order[b]
+    const uint32_t tl = fa.order[blockIdx.y * gridDim.x + blockIdx.x];
+    bx = tl % gridDim.x;
+    by = tl / gridDim.x;
+  }
+  const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
+  const int xo = bx * kTile + (wave & 1) * 8 + (lane & 7);
+  const int yl = by * kTile + (wave >> 1) * 8 + (lane >> 3);
   const bool active = xo < fa.W && yl < fa.rows_local;
   if (DIAG == 0 && !active) return;
   if (active) {  // (the counting variant keeps every lane for its wave reduction)
@@ -301,6 +310,13 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
       fb_store(fa.t + idx, t);
     }
   }
+  if constexpr (DIAG == 0) {
+    if (fa.cost) {  // this wave's duration; the tile keeps its slowest wave's
+      const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
+      if (lane == __ffsll((unsigned long long)__ballot(1)) - 1)
+        atomicMax(fa.cost + by * gridDim.x + bx, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt);
+    }
+  }
   if constexpr (DIAG == 1) flush_counts(cnt, counters);
   if constexpr (DIAG == 2) {
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -325,97 +341,6 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
   }
 }
 
-// ---- two-kernel (wavefront) primary path for meshes -------------------------
-// Renderer::draw with Normal shading and no plane, split at the root: K1 does
-// ray generation and the root stage for every pixel, resolves the rays that
-// enter no root child (86% at 1080p on the bunny), and compacts the others into
-// a queue (wave ballot + prefix count, one atomic per wave); K2 traces only the
-// queued rays. Heavy rays then all start together at the top of K2 instead of
-// being spread over a long dispatch that is mostly trivial waves.
-struct alignas(16) QEntry {
-  uint32_t pix;      // yl * W + xo (packed-row index)
-  float dx, dy, dz;  // world ray direction
-  uint32_t list;     // root frame: remaining children | count << 24
-  float tfirst;      // entry t of the first child
-  uint32_t cwfirst;  // child word of the first child
-  float tfar;        // std::min(100, tPrev)
-};
-
-__device__ __forceinline__ f4 normal_color(f3 n, f3 d) {
-  if (dot(n, d) > 0) n = n * -1.0f;
-  return f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
-}
-
-__global__ __launch_bounds__(kBlock) void mesh_primary_k1(MeshDev sc, FrameArgs fa, QEntry *q,
-                                                          uint32_t *qcount) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int xo = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-  const int yl = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
-  const bool active = xo < fa.W && yl < fa.rows_local;
-  bool survive = false;
-  QEntry e;
-  if (active) {
-    const int yo = image_row(yl, fa);
-    const int y = fa.H - yo - 1;
-    const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
-    const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
-    const size_t idx = (size_t)yl * fa.W + xo;
-    const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
-    const float tPrev = clear ? kInf : fa.t[idx];
-    const float tFarEff = std_min(100.0f, tPrev);
-    const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    uint32_t l = 0, c = 0, cwf = 0;
-    float tf = 0.0f;
-    NoCnt nc;
-    survive = mesh_root(sc, o, inv, 0.01f, tFarEff, l, c, tf, cwf, nc);
-    if (survive) {
-      e = QEntry{(uint32_t)idx, d.x, d.y, d.z, l | (c << 24), tf, cwf, tFarEff};
-    } else if (clear) {
-      fa.color[idx] = 0u;
-      fa.t[idx] = kInf;
-    }
-  }
-  const unsigned long long m = __ballot(survive);
-  if (m == 0) return;
-  const uint32_t n = (uint32_t)__popcll(m);
-  const int leader = __builtin_ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(qcount, n);
-  base = (uint32_t)__shfl((int)base, leader, 64);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  if (survive) q[base + rank] = e;
-}
-
-template <int SLOTS>
-__global__ __launch_bounds__(kBlock) void mesh_primary_k2(MeshDev sc, FrameArgs fa, const QEntry *q,
-                                                          const uint32_t *qcount) {
-  __shared__ uint32_t stk[SLOTS * 3 * kBlock];
-  LdsStack<kBlock> st{stk + threadIdx.x};
-  const uint32_t n = *qcount;
-  const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
-  NoCnt nc;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const QEntry e = q[i];
-    const f3 d{e.dx, e.dy, e.dz};
-    const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    float t;
-    uint32_t k;
-    const bool hit = mesh_continue<kBlock, false>(sc, o, d, inv, 0.01f, e.tfar, st, rtl::kInvalidChild,
-                                                  e.list & 0xFFFFFFu, e.list >> 24, e.tfirst, e.cwfirst,
-                                                  true, 1, t, k, nc);
-    const bool store = hit && !__builtin_isinf(t);
-    const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
-    if (store) {
-      fa.color[e.pix] = pack_rgba(normal_color(tri_normal(sc.tris, k), d));
-      fa.t[e.pix] = t;
-    } else if (clear) {
-      fa.color[e.pix] = 0u;
-      fa.t[e.pix] = kInf;
-    }
-  }
-}
-
-// IScene::intersect over a batch of rays (union with the plane if enabled).
 template <class S, int SLOTS>
 __global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const float *o3,
                                                        const float *d3, int64_t n, float tn,
@@ -448,6 +373,39 @@ __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_r
   if (t) t[i] = pt[src];
 }
 
+// Block schedule for the next frame from this frame's per-tile costs:
+// tiles in descending cost class (2 classes per octave of shader cycles), so
+// the long-running tiles of a frame -- grazing rays at silhouettes, the tail
+// that otherwise starts late and runs alone -- are dispatched first. Order
+// within a class is arbitrary; the image does not depend on the order. Resets
+// the costs for the next frame.
+constexpr int kCostClasses = 66;
+__device__ __forceinline__ uint32_t cost_class(uint32_t c) {
+  if (c == 0) return 0;
+  const uint32_t e = 32u - (uint32_t)__clz(c);
+  return 2 * e + (e >= 2 ? (c >> (e - 2)) & 1u : 0u);
+}
+__global__ __launch_bounds__(1024) void order_kernel(uint32_t *cost, uint32_t *order, uint32_t n) {
+  __shared__ uint32_t hist[kCostClasses];
+  for (uint32_t i = threadIdx.x; i < kCostClasses; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_class(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int b = kCostClasses - 1; b >= 0; --b) {
+      const uint32_t h = hist[b];
+      hist[b] = run;
+      run += h;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    order[atomicAdd(&hist[cost_class(cost[i])], 1u)] = i;
+    cost[i] = 0;
+  }
+}
+
 }  // namespace
 
 // ================================================================== C ABI ==
@@ -475,18 +433,26 @@ struct rt_scene {
   uint32_t *d_color = nullptr;
   float *d_t = nullptr;
   size_t fb_cap = 0;
-  // wavefront queue (mesh primary path), sized to the largest frame rendered
-  QEntry *d_queue = nullptr;
-  uint32_t *d_qcount = nullptr;
-  size_t q_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // A/B switch: two-kernel wavefront primary path. Off by default: measured
-  // slower (bunny 1080p 0.417 vs 0.330 ms): concentrating the heavy rays in
-  // K2 raises their memory latency more than it saves in scheduling.
-  bool use_wavefront = false;
+  // cost-ordered block schedule (see launch_render): per-block cost of the
+  // last frame rendered with sched_grid blocks, and the block order derived
+  // from it; sched_on = false renders in plain blockIdx order
+  uint32_t *d_cost = nullptr;
+  uint32_t *d_order = nullptr;
+  uint32_t sched_cap = 0;
+  uint32_t sched_grid = 0;
+  bool sched_on = true;
+  hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
+  hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
 };
 
 namespace {
+
+GridDev grid_dev(const rt_scene *s) {
+  const uint64_t n = (uint64_t)s->size[0] * s->size[1] * s->size[2];
+  return GridDev{s->d_vals, s->size[0], s->size[1], s->size[2], s->size[1] * s->size[2], n <= (1ull << 24),
+                 4 * n < (1ull << 31) ? (uint32_t)(4 * n) : 0u};
+}
 
 MeshDev mesh_dev(const rt_scene *s) {
   MeshDev m{s->d_nodes, s->d_tris, s->root, {}};
@@ -546,44 +512,57 @@ void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool 
   }
 }
 
-int ensure_queue(rt_scene *s, size_t n) {
-  if (n <= s->q_cap) return RT_OK;
-  if (s->d_queue) (void)hipFree(s->d_queue);
-  s->d_queue = nullptr;
-  s->q_cap = 0;
-  HIP_TRY(hipMalloc(&s->d_queue, n * sizeof(QEntry)));
-  if (!s->d_qcount) HIP_TRY(hipMalloc(&s->d_qcount, 64));
-  s->q_cap = n;
-  return RT_OK;
-}
-
-int launch_mesh_primary(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
-  const size_t px = (size_t)fa.W * fa.rows_local;
-  int rc = ensure_queue(s, px);
-  if (rc) return rc;
-  HIP_TRY(hipMemsetAsync(s->d_qcount, 0, 4, stream));
-  const MeshDev md = mesh_dev(s);
-  const dim3 g1((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
-  mesh_primary_k1<<<g1, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount);
-  // K2: enough workgroups to hold every queued ray in one pass when they fit
-  // the machine, grid-stride beyond that.
-  const unsigned g2 = (unsigned)std::min<size_t>((px + kBlock - 1) / kBlock, 4096);
-  switch (s->maxd) {
-    case 4: mesh_primary_k2<4><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
-    case 7: mesh_primary_k2<7><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
-    case 15: mesh_primary_k2<15><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
-    default: mesh_primary_k2<31><<<g2, kBlock, 0, stream>>>(md, fa, s->d_queue, s->d_qcount); break;
+// Cost-ordered schedule state for a frame of grid gx x gy blocks on `stream`.
+// Renders of one scene on different streams are ordered through sched_ev, so
+// the order/cost buffers are never shared by two frames in flight.
+int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
+  fa.order = nullptr;
+  fa.cost = nullptr;
+  if (!s->sched_on) return RT_OK;
+  const uint32_t nb = gx * gy;
+  if (nb > s->sched_cap) {
+    if (s->d_cost) (void)hipFree(s->d_cost);
+    if (s->d_order) (void)hipFree(s->d_order);
+    s->d_cost = s->d_order = nullptr;
+    s->sched_cap = 0;
+    s->sched_grid = 0;
+    if (s->sched_ev) HIP_TRY(hipEventSynchronize(s->sched_ev));
+    HIP_TRY(hipMalloc(&s->d_cost, (size_t)nb * 4));
+    HIP_TRY(hipMalloc(&s->d_order, (size_t)nb * 4));
+    HIP_TRY(hipMemset(s->d_cost, 0, (size_t)nb * 4));
+    s->sched_cap = nb;
   }
-  HIP_TRY(hipGetLastError());
+  if (!s->sched_ev) HIP_TRY(hipEventCreateWithFlags(&s->sched_ev, hipEventDisableTiming));
+  if (stream != s->sched_stream) {
+    HIP_TRY(hipStreamWaitEvent(stream, s->sched_ev, 0));
+    s->sched_stream = stream;
+  }
+  const uint32_t key = (gx << 16) | gy;
+  if (s->sched_grid == key) fa.order = s->d_order;
+  fa.cost = s->d_cost;
   return RT_OK;
 }
 
-int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream,
+int schedule_end(rt_scene *s, const FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
+  if (!fa.cost) return RT_OK;
+  order_kernel<<<1, 1024, 0, stream>>>(s->d_cost, s->d_order, gx * gy);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(s->sched_ev, stream));
+  s->sched_grid = (gx << 16) | gy;
+  return RT_OK;
+}
+
+int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
                   unsigned long long *counters = nullptr, int diag = 0) {
+  FrameArgs fa = fa_in;
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
-  if (s->kind == RT_SCENE_MESH && !general && diag == 0 && s->root != rtl::kInvalidChild &&
-      !(s->root & rtl::kLeafBit) && s->use_wavefront)
-    return launch_mesh_primary(s, fa, stream);
+  const uint32_t gx = (fa.W + kTile - 1) / kTile, gy = (fa.rows_local + kTile - 1) / kTile;
+  fa.order = nullptr;
+  fa.cost = nullptr;
+  if (diag == 0) {
+    const int rc = schedule_begin(s, fa, gx, gy, stream);
+    if (rc) return rc;
+  }
   if (s->kind == RT_SCENE_MESH) {
     MeshS sc{mesh_dev(s)};
     switch (s->maxd) {
@@ -593,7 +572,7 @@ int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream,
       default: launch_render_t<MeshS, 31>(sc, s->plane, fa, general, stream, counters, diag); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
-    GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
+    GridS sc{grid_dev(s)};
     launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream, counters, diag);
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
@@ -607,6 +586,7 @@ int launch_render(rt_scene *s, const FrameArgs &fa, hipStream_t stream,
     return set_err(RT_E_STATE, "scene has no geometry");
   }
   HIP_TRY(hipGetLastError());
+  if (diag == 0) return schedule_end(s, fa, gx, gy, stream);
   return RT_OK;
 }
 
@@ -879,9 +859,10 @@ int rt_scene_destroy(rt_scene *s) {
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(s->device);
   void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t,
-                  s->d_queue, s->d_qcount};
+                  s->d_cost, s->d_order};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  if (s->sched_ev) (void)hipEventDestroy(s->sched_ev);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   (void)hipSetDevice(prev);
@@ -977,7 +958,7 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
         default: launch_rays_t<MeshS, 31>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     } else if (s->kind == RT_SCENE_GRID) {
-      GridS sc{GridDev{s->d_vals, s->size[0], s->size[1], s->size[2]}};
+      GridS sc{grid_dev(s)};
       launch_rays_t<GridS, 1>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP);
     } else {
       OctS sc{OctDev{s->d_child, s->d_ovals}};
@@ -1051,10 +1032,11 @@ int rtx_wave_stamps(rt_scene *s, const rt_render_params *params, int32_t W, int3
   return RT_OK;
 }
 
-// Diagnostic: two-kernel wavefront path for mesh primary rays (A/B).
-int rtx_set_wavefront(rt_scene *s, int on) {
+// Diagnostic A/B switch: cost-ordered block schedule on (default) / off.
+int rtx_set_schedule(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
-  s->use_wavefront = on != 0;
+  s->sched_on = on != 0;
+  s->sched_grid = 0;
   return RT_OK;
 }
 

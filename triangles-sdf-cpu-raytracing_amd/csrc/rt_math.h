@@ -59,6 +59,28 @@ __device__ __forceinline__ float slab_ispc(float bx0, float by0, float bz0, floa
   return (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
 }
 
+// slab_ispc when no operand can be NaN (every 1/d component finite, hence
+// nonzero; box bounds finite or +inf): ISPC's MINPS/MAXPS forms then equal
+// IEEE min/max (signed zeros aside, and a zero entry distance is only ever
+// compared, never used arithmetically), and min/max are associative, so the
+// hardware's 2- and 3-operand v_min/v_max give the same bits in fewer ops.
+__device__ __forceinline__ float slab_fast(float bx0, float by0, float bz0, float bx1, float by1,
+                                           float bz1, f3 o, f3 inv, float tNear, float tFar) {
+  const float t1x = (bx0 - o.x) * inv.x, t1y = (by0 - o.y) * inv.y, t1z = (bz0 - o.z) * inv.z;
+  const float t2x = (bx1 - o.x) * inv.x, t2y = (by1 - o.y) * inv.y, t2z = (bz1 - o.z) * inv.z;
+  const float tMin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)),
+                                     __builtin_fmaxf(__builtin_fminf(t1z, t2z), tNear));
+  const float tMax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)),
+                                     __builtin_fminf(__builtin_fmaxf(t1z, t2z), tFar));
+  return (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
+}
+template <bool FAST>
+__device__ __forceinline__ float slab(float bx0, float by0, float bz0, float bx1, float by1, float bz1,
+                                      f3 o, f3 inv, float tNear, float tFar) {
+  return FAST ? slab_fast(bx0, by0, bz0, bx1, by1, bz1, o, inv, tNear, tFar)
+              : slab_ispc(bx0, by0, bz0, bx1, by1, bz1, o, inv, tNear, tFar);
+}
+
 // LiteMath BBox3f::Intersection restatement:
 // t1 = max(tmin, max3(min(lo,hi))), t2 = min(tmax, min3(max(lo,hi))), std semantics.
 __device__ __forceinline__ void bbox_intersection(f3 bmin, f3 bmax, f3 o, f3 inv, float tmin,

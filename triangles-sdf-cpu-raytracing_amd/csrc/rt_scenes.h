@@ -115,6 +115,7 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
 // (a suffix of the sorted order) as a packed list of 3-bit ids + count. Also
 // returns the entry distance and child word of the first child to visit (the
 // child words arrive with the boxes: descending needs no extra load).
+template <bool FAST>
 __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node, f3 o, f3 inv,
                                             float tNear, float tFar, uint32_t &list,
                                             uint32_t &cnt, float &tfirst, uint32_t &cwfirst) {
@@ -132,7 +133,7 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    t[c] = slab_ispc(bx[6 * c], bx[6 * c + 1], bx[6 * c + 2], bx[6 * c + 3], bx[6 * c + 4],
+    t[c] = slab<FAST>(bx[6 * c], bx[6 * c + 1], bx[6 * c + 2], bx[6 * c + 3], bx[6 * c + 4],
                      bx[6 * c + 5], o, inv, tNear, tFar);
     id[c] = (uint32_t)c;
   }
@@ -181,18 +182,18 @@ __device__ __forceinline__ bool root_box_miss(const float *b, f3 o, f3 inv, floa
 // Root stage of BVHBuilder::traverseNode(0): the union-box pretest and the
 // root's 8-child expansion (wave-uniform node: scalar loads). Returns false if
 // the traversal ends here (no child entered); otherwise the root frame.
-template <class CT>
+template <bool FAST = false, class CT>
 __device__ __forceinline__ bool mesh_root(const MeshDev &sc, f3 o, f3 inv, float tNear, float tFar,
                                           uint32_t &l, uint32_t &c, float &tf, uint32_t &cwf,
                                           CT &cnt) {
   cnt.add(C_BVH_INNER, 1);
   if (root_box_miss(sc.rbox, o, inv, tNear, tFar)) return false;
-  expand_node(sc.nodes + sc.root, o, inv, tNear, tFar, l, c, tf, cwf);
+  expand_node<FAST>(sc.nodes + sc.root, o, inv, tNear, tFar, l, c, tf, cwf);
   return c != 0;
 }
 
 // Traversal below the root frame (or from a root leaf when root_is_leaf).
-template <int BLOCK, bool ANY, class CT>
+template <int BLOCK, bool ANY, bool FAST = false, class CT>
 __device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear,
                                               float tFar, LdsStack<BLOCK> st, uint32_t word,
                                               uint32_t flist, uint32_t fcnt, float tnext,
@@ -221,7 +222,7 @@ __device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 
         uint32_t l, c, cwf;
         float tf;
         cnt.add(C_BVH_INNER, 1);
-        expand_node(sc.nodes + word, o, inv, tNear, tFar, l, c, tf, cwf);
+        expand_node<FAST>(sc.nodes + word, o, inv, tNear, tFar, l, c, tf, cwf);
         if (c != 0) {
           if (depth >= 1) {
             st.at(depth - 1, 0) = fnode;
@@ -258,7 +259,7 @@ __device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 
       const rtl::GNode *nd = sc.nodes + fnode;
       const float *b = nd->box[j];
       cwnext = nd->child[j];
-      tnext = slab_ispc(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
+      tnext = slab<FAST>(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
     }
     have_t = false;
     if (fbest < tnext) { fcnt = 0; continue; }  // pruned; later siblings have larger t
@@ -280,9 +281,14 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
                                      rtl::kInvalidChild, false, 0, out_t, out_k, cnt);
   uint32_t l, c, cwf;
   float tf;
-  if (!mesh_root(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)) return false;
-  return mesh_continue<BLOCK, ANY>(sc, o, d, inv, tNear, tFar, st, rtl::kInvalidChild, l, c, tf, cwf,
-                                   true, 1, out_t, out_k, cnt);
+  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z)) {
+    if (!mesh_root<true>(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)) return false;
+    return mesh_continue<BLOCK, ANY, true>(sc, o, d, inv, tNear, tFar, st, rtl::kInvalidChild, l, c, tf,
+                                           cwf, true, 1, out_t, out_k, cnt);
+  }
+  if (!mesh_root<false>(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)) return false;
+  return mesh_continue<BLOCK, ANY, false>(sc, o, d, inv, tNear, tFar, st, rtl::kInvalidChild, l, c, tf,
+                                          cwf, true, 1, out_t, out_k, cnt);
 }
 
 template <int BLOCK, class CT>
@@ -313,7 +319,13 @@ __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, flo
 struct GridDev {
   const float *__restrict__ v;
   uint32_t sx, sy, sz;
+  uint32_t syz;    // sy * sz
+  bool small;      // sx * sy * sz <= 2^24: 24-bit multiplies are exact for every index
+  uint32_t bytes;  // 4 * sx * sy * sz when < 2^32 (buffer-load path with 32-bit offsets), else 0
 };
+
+// gfx9 buffer resource word 3 (raw dword access, no swizzle)
+constexpr int kBufWord3 = 0x00020000;
 
 template <class CT>
 __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell, CT &cnt) {
@@ -329,10 +341,32 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   if (i1x == i0x) { ax = 1.0f; bx = 0.0f; }
   if (i1y == i0y) { ay = 1.0f; by = 0.0f; }
   if (i1z == i0z) { az = 1.0f; bz = 0.0f; }
-  const uint32_t r00 = (i0x * g.sy + i0y) * g.sz, r01 = (i0x * g.sy + i1y) * g.sz;
-  const uint32_t r10 = (i1x * g.sy + i0y) * g.sz, r11 = (i1x * g.sy + i1y) * g.sz;
-  const float p0 = g.v[r00 + i0z], p1 = g.v[r00 + i1z], p2 = g.v[r01 + i0z], p3 = g.v[r01 + i1z];
-  const float p4 = g.v[r10 + i0z], p5 = g.v[r10 + i1z], p6 = g.v[r11 + i0z], p7 = g.v[r11 + i1z];
+  // the 8 taps (x*sy+y)*sz+z (grid_raytracing.hpp:13-15) as one base index plus
+  // per-axis steps of 0 (c1 == c0) or one sample
+  const uint32_t base = g.small ? __umul24(__umul24(i0x, g.sy) + i0y, g.sz) + i0z
+                                : (i0x * g.sy + i0y) * g.sz + i0z;
+  const uint32_t dz = i1z - i0z;
+  const uint32_t dy = i1y != i0y ? g.sz : 0u;
+  const uint32_t dx = i1x != i0x ? g.syz : 0u;
+  float p0, p1, p2, p3, p4, p5, p6, p7;
+  if (g.bytes) {  // buffer loads: 32-bit byte offsets, no 64-bit address arithmetic
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.v), 0, (int)g.bytes, kBufWord3);
+    const uint32_t o0 = base << 2, z4 = dz << 2, y4 = dy << 2, o4 = o0 + (dx << 2);
+    p0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0, 0, 0));
+    p1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + z4, 0, 0));
+    p2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + y4, 0, 0));
+    p3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + y4 + z4, 0, 0));
+    p4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4, 0, 0));
+    p5 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + z4, 0, 0));
+    p6 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + y4, 0, 0));
+    p7 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + y4 + z4, 0, 0));
+  } else {
+    const float *__restrict__ v0 = g.v + base;
+    const float *__restrict__ v1 = v0 + dx;
+    p0 = v0[0]; p1 = v0[dz]; p2 = v0[dy]; p3 = v0[dy + dz];
+    p4 = v1[0]; p5 = v1[dz]; p6 = v1[dy]; p7 = v1[dy + dz];
+  }
   float res = 0.0f;
   res += p0 * bx * by * bz;
   res += p1 * bx * by * az;
@@ -342,7 +376,7 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   res += p5 * ax * by * az;
   res += p6 * ax * ay * bz;
   res += p7 * ax * ay * az;
-  if (cell) *cell = r00 + i0z;
+  if (cell) *cell = base;
   return res;
 }
 
