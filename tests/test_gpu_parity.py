@@ -178,3 +178,50 @@ def test_golden_fixture_frames(gpu):
         name, W, H, mode, pos = case
         c, t = S.gpu_frame(name, W, H, mode, pos)
         assert_same((data[ent["color"]], data[ent["t"]]), (c, t), ent["case"])
+
+
+def test_schedule_state_is_output_neutral(gpu):
+    """The cost-ordered block schedule (per-scene state carried from frame to
+    frame) never changes the image: frames rendered while alternating frame
+    sizes, row-band tiles, two HIP streams and the schedule switch equal the
+    oracle / each other bit for bit."""
+    import ctypes as C
+
+    import rtamd
+    from rtamd._lib import lib
+    torch = pytest.importorskip("torch")
+    from rtamd.workloads import orbit_positions
+    L = lib()
+    L.rtx_set_schedule.argtypes = [C.c_void_p, C.c_int]
+    name = "stanford-bunny.obj"
+    s = S.gpu_scene(name)
+    S.set_planes(name, "primary", s)
+    sizes = [(320, 180), (256, 256), (320, 180)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = {}
+    for rep in range(2):
+        L.rtx_set_schedule(s._h, rep)  # rep 0: off, rep 1: on (state reused across frames)
+        for k, pos in enumerate(orbit_positions(64)[:6]):
+            W, H = sizes[k % 3]
+            P = S.params(name, W, H, "primary", pos, module="gpu")
+            c = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+            t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+            st = streams[k % 2]
+            with torch.cuda.stream(st):
+                s.render_device(P, c.data_ptr(), t.data_ptr(), W, H, clear=True, stream=st.cuda_stream)
+                if k % 2 == 1:  # a row-band tile frame in between, on the same scene
+                    tile = rtamd.Tile(16, 1, 3, 0)
+                    n = L.rt_tile_pixels(W, H, C.byref(tile))
+                    pc = torch.zeros(n, dtype=torch.int32, device="cuda")
+                    pt = torch.zeros(n, dtype=torch.float32, device="cuda")
+                    s.render_device(P, pc.data_ptr(), pt.data_ptr(), W, H, clear=True, tile=tile,
+                                    stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            outs[(rep, k)] = (c.cpu().numpy().view(np.uint32), t.cpu().numpy())
+    L.rtx_set_schedule(s._h, 1)
+    for k, pos in enumerate(orbit_positions(64)[:6]):
+        W, H = sizes[k % 3]
+        for rep in range(2):
+            assert np.array_equal(outs[(rep, k)][0], outs[(0, k)][0])
+        if k < 3:
+            assert_same(S.ref_frame(name, W, H, "primary", pos), outs[(1, k)], f"schedule frame {k}")
