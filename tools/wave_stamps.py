@@ -53,6 +53,13 @@ print(f"  waves ending in the last 30% of the span: {late.sum()}, start p10/p50/
       f"{np.percentile(st[late], 90)/1e3:.1f} us, duration p50 {np.percentile(dur[late], 50)/1e3:.1f} us")
 print(f"  SIMD efficiency (sum / 64*max over waves): {smu.sum() / max(64*mxu.sum(),1):.3f}")
 xcc = buf[:, 3] & 0xF
+u9 = (buf[:, 3] >> np.uint64(8)).astype(np.int64)
+heavy = mxu > 40
+print(f"  waves with max units > 40: {heavy.sum()}; their units done with >8 lanes busy (u9/max): "
+      f"p10/p50/p90 {np.percentile(u9[heavy]/mxu[heavy],10):.2f}/{np.percentile(u9[heavy]/mxu[heavy],50):.2f}/"
+      f"{np.percentile(u9[heavy]/mxu[heavy],90):.2f}")
+for i in order:
+    print(f"    slow wave: max {mxu[i]} u9 {u9[i]} sum {smu[i]}")
 for x in range(8):
     m = xcc == x
     if m.any():

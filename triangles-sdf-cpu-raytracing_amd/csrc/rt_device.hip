@@ -54,7 +54,22 @@ struct FrameArgs {
 // octree: node, list|count; grid: none).
 struct MeshS {
   static constexpr int kFields = 3;
+  static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   MeshDev d;
+  template <int B>
+  __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
+                                         uint32_t *stk) const {
+    float t;
+    uint32_t k;
+    Hit h = miss_hit();
+    if (mesh_primary_wave<B>(d, o, dir, tn, tf, active, stk, t, k) && active) {
+      h.hit = true;
+      h.t = t;
+      h.n = tri_normal(d.tris, k);
+      h.prim = (int64_t)d.tris[k].orig_id;
+    }
+    return h;
+  }
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields> st, CT &cnt) const {
@@ -68,6 +83,7 @@ struct MeshS {
 };
 struct GridS {
   static constexpr int kFields = 1;
+  static constexpr bool kCoop = false;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -82,6 +98,7 @@ struct GridS {
 };
 struct OctS {
   static constexpr int kFields = 2;
+  static constexpr bool kCoop = false;
   OctDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -275,23 +292,29 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
   const int xo = bx * kTile + (wave & 1) * 8 + (lane & 7);
   const int yl = by * kTile + (wave >> 1) * 8 + (lane >> 3);
   const bool active = xo < fa.W && yl < fa.rows_local;
-  if (DIAG == 0 && !active) return;
-  if (active) {  // (the counting variant keeps every lane for its wave reduction)
+  // wave-cooperative primary path: every lane of the wave takes part
+  constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
+  if (DIAG == 0 && !kWaveCoop && !active) return;
+  if (active || kWaveCoop) {  // (the counting variant keeps every lane for its wave reduction)
     LdsStack<kBlock, S::kFields> st{stk + threadIdx.x};
-    const int yo = image_row(yl, fa);
+    const int yo = image_row(active ? yl : 0, fa);
     const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
     const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
-    const f3 d = eye_ray(xo, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
-    const size_t idx = (size_t)yl * fa.W + xo;
+    const f3 d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+    const size_t idx = active ? (size_t)yl * fa.W + xo : 0;
     const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
-    const float tPrev = clear ? kInf : fa.t[idx];
+    const float tPrev = (clear || !active) ? kInf : fa.t[idx];
     const float tFarEff = std_min(100.0f, tPrev);  // std::min(tFar, tPrev)
     bool hit;
     float t;
     f4 c;
     if (!GENERAL) {
       cnt.add(C_RAYS, 1);
-      const Hit h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st, cnt);
+      Hit h;
+      if constexpr (kWaveCoop)
+        h = sc.template primary<kBlock>(o, d, 0.01f, tFarEff, active, stk);
+      else
+        h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st, cnt);
       hit = h.hit;
       t = h.t;
       f3 n = h.n;
@@ -302,7 +325,9 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
     }
     // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
     const bool store = hit && !__builtin_isinf(t);
-    if (clear) {
+    if (!active) {
+      // helper lane of the cooperative path: no pixel of its own
+    } else if (clear) {
       fb_store(fa.color + idx, store ? pack_rgba(c) : 0u);
       fb_store(fa.t + idx, store ? t : kInf);
     } else if (store) {
@@ -331,12 +356,26 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
       mx = mx > om ? mx : om;
       sm += os;
     }
+    // the 9th-largest lane's units: the work the wave does with more than 8 lanes busy
+    uint32_t rest = units, u9 = 0;
+    for (int r = 0; r < 9; ++r) {
+      uint32_t m = rest;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t om = __shfl_xor(m, off, 64);
+        m = m > om ? m : om;
+      }
+      u9 = m;
+      const uint64_t who = __ballot(rest == m);
+      if ((threadIdx.x & 63) == (int)__builtin_ctzll(who)) rest = 0;
+    }
     if ((threadIdx.x & 63) == 0) {
       const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
       counters[4 * w] = t_start;
       counters[4 * w + 1] = t_end;
       counters[4 * w + 2] = ((unsigned long long)sm << 32) | mx;
-      counters[4 * w + 3] = __builtin_amdgcn_s_getreg(0x1814);  // HW_REG_XCC_ID, 4 bits
+      // HW_REG_XCC_ID (4 bits) | 9th-largest lane units << 8
+      counters[4 * w + 3] = __builtin_amdgcn_s_getreg(0x1814) | ((unsigned long long)u9 << 8);
     }
   }
 }

@@ -193,28 +193,48 @@ __device__ __forceinline__ bool mesh_root(const MeshDev &sc, f3 o, f3 inv, float
 }
 
 // Traversal below the root frame (or from a root leaf when root_is_leaf).
-template <int BLOCK, bool ANY, bool FAST = false, class CT>
-__device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear,
-                                              float tFar, LdsStack<BLOCK> st, uint32_t word,
-                                              uint32_t flist, uint32_t fcnt, float tnext,
-                                              uint32_t cwnext, bool have_t, int depth,
-                                              float &out_t, uint32_t &out_k, CT &cnt) {
-  float gbest = kInf;
-  uint32_t gk = rtl::kInvalidChild;
-  // top frame in registers; frames below it in LDS slots [0, depth-2]
-  uint32_t fnode = sc.root;
-  float fbest = kInf;
-  // One loop iteration = one unit of this lane's work (expand a node, test a
-  // leaf, or resume/pop a frame). (Measured and rejected: the "while-while"
-  // split into an inner-node phase and a leaf phase: bunny 0.342 -> 0.523 ms.)
+// Traversal state of one ray below its root frame. The top frame lives in
+// registers, the frames below it in LDS slots [0, depth-2].
+struct MState {
+  uint32_t word;    // next node/leaf to process (kInvalidChild: none)
+  uint32_t flist;   // top frame: remaining child ids, 3 bits each, next in the low bits
+  uint32_t fcnt;    // top frame: remaining child count
+  uint32_t fnode;   // top frame: node index
+  uint32_t cwnext;  // child word of the next child (valid with have_t)
+  uint32_t gk;      // best triangle slot so far (kInvalidChild: none)
+  float fbest;      // top frame's LOCAL best t
+  float tnext;      // entry t of the next child (valid with have_t)
+  float gbest;      // best t so far
+  int32_t depth;    // frames on the stack, incl. the top one
+  bool have_t;
+};
+
+// Rays still looping in a wave at or below which the primary mesh path hands
+// its remaining rays to 8-lane groups (mesh_run_coop).
+constexpr int kCoopRays = 8;
+
+// The traversal loop. One iteration = one unit of this lane's work (expand a
+// node, test a leaf, or resume/pop a frame). (Measured and rejected: the
+// "while-while" split into an inner-node phase and a leaf phase: bunny
+// 0.342 -> 0.523 ms.) TAIL: before each iteration, if kCoopRays or fewer lanes
+// of the wave are still looping, store the state and return true (suspended).
+template <int BLOCK, bool ANY, bool FAST, bool TAIL, class CT>
+__device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
+                                         LdsStack<BLOCK> st, MState &S, CT &cnt) {
+  uint32_t word = S.word, flist = S.flist, fcnt = S.fcnt, fnode = S.fnode, cwnext = S.cwnext, gk = S.gk;
+  float fbest = S.fbest, tnext = S.tnext, gbest = S.gbest;
+  int depth = S.depth;
+  bool have_t = S.have_t;
+  bool suspended = false;
   for (;;) {
+    if (TAIL && __popcll(__ballot(1)) <= kCoopRays) { suspended = true; break; }
     if (word != rtl::kInvalidChild) {
       if (word & rtl::kLeafBit) {
         float lt = kInf;
         uint32_t lk = rtl::kInvalidChild;
         leaf_test(sc.tris, word, o, d, lt, lk, cnt);
         if (lk != rtl::kInvalidChild) {
-          if (ANY) { out_t = lt; out_k = lk; return true; }
+          if (ANY) { gbest = lt; gk = lk; break; }
           if (lt < fbest) fbest = lt;
           if (lt < gbest) { gbest = lt; gk = lk; }
         }
@@ -265,9 +285,272 @@ __device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 
     if (fbest < tnext) { fcnt = 0; continue; }  // pruned; later siblings have larger t
     word = cwnext;
   }
-  out_t = gbest;
-  out_k = gk;
-  return gk != rtl::kInvalidChild;
+  S.word = word; S.flist = flist; S.fcnt = fcnt; S.fnode = fnode; S.cwnext = cwnext; S.gk = gk;
+  S.fbest = fbest; S.tnext = tnext; S.gbest = gbest; S.depth = depth; S.have_t = have_t;
+  return suspended;
+}
+
+template <int BLOCK, bool ANY, bool FAST = false, class CT>
+__device__ __forceinline__ bool mesh_continue(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear,
+                                              float tFar, LdsStack<BLOCK> st, uint32_t word,
+                                              uint32_t flist, uint32_t fcnt, float tnext,
+                                              uint32_t cwnext, bool have_t, int depth,
+                                              float &out_t, uint32_t &out_k, CT &cnt) {
+  MState S{word, flist, fcnt, sc.root, cwnext, rtl::kInvalidChild, kInf, tnext, kInf, depth, have_t};
+  mesh_run<BLOCK, ANY, FAST, false>(sc, o, d, inv, tNear, tFar, st, S, cnt);
+  out_t = S.gbest;
+  out_k = S.gk;
+  return S.gk != rtl::kInvalidChild;
+}
+
+// ---- 8-lane groups: the cooperative tail of the primary mesh path ---------
+// When at most kCoopRays rays of a wave are still traversing (the long,
+// grazing ones that otherwise run alone on an idle wave), each gets a group of
+// 8 lanes -- one DPP half-row, lanes 8g..8g+7, k = lane & 7 -- and the group
+// runs the SAME traversal (same visiting order, same local-best pruning, same
+// arithmetic) with the per-node work spread over its lanes: lane k slab-tests
+// child k, the sort8 network runs across the lanes (its 19 comparators in 7
+// layers, exchanged through DPP), and lane k tests triangle k of a leaf
+// followed by a first-wins min reduction. Everything else (frame push/pop,
+// resume, prune) is executed identically by the 8 lanes on the owner lane's
+// LDS stack.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v)));
+}
+// DPP controls: quad_perm [1,0,3,2], [2,3,0,1], [0,2,1,3]; row_shl:n (lane i
+// reads lane i+n) = 0x100+n, row_shr:n (lane i reads lane i-n) = 0x110+n.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppSwap12 = 0xD8;
+template <int N> constexpr int kDppShl = 0x100 + N;
+template <int N> constexpr int kDppShr = 0x110 + N;
+
+// One comparator of sort8 seen from one of its two lanes: swap iff
+// t[lower] > t[upper] (RTD_CSWAP), identical on both lanes.
+__device__ __forceinline__ void grp_cswap(float &t, uint32_t &id, float pt, uint32_t pid, bool in,
+                                          bool lower) {
+  const bool sw = in && (lower ? (t > pt) : (pt > t));
+  t = sw ? pt : t;
+  id = sw ? pid : id;
+}
+// A comparator layer whose pairs are (k, k+N) for the lanes in it.
+template <int N>
+__device__ __forceinline__ void grp_layer_shift(float &t, uint32_t &id, bool in, bool lower) {
+  const float tl = dpp_f<kDppShl<N>>(t), tr = dpp_f<kDppShr<N>>(t);
+  const uint32_t il = dpp_u<kDppShl<N>>(id), ir = dpp_u<kDppShr<N>>(id);
+  grp_cswap(t, id, lower ? tl : tr, lower ? il : ir, in, lower);
+}
+// sort8 (raytracing.hpp:188-213) over the group: lane k holds entry k.
+__device__ __forceinline__ void grp_sort8(float &t, uint32_t &id, int k) {
+  // (0,1)(2,3)(4,5)(6,7)
+  grp_cswap(t, id, dpp_f<kDppXor1>(t), dpp_u<kDppXor1>(id), true, (k & 1) == 0);
+  // (0,2)(1,3)(4,6)(5,7)
+  grp_cswap(t, id, dpp_f<kDppXor2>(t), dpp_u<kDppXor2>(id), true, (k & 2) == 0);
+  {  // (1,2)(5,6)(0,4)(3,7)
+    const bool mid = k == 1 || k == 2 || k == 5 || k == 6;
+    const float tq = dpp_f<kDppSwap12>(t), tl = dpp_f<kDppShl<4>>(t), tr = dpp_f<kDppShr<4>>(t);
+    const uint32_t iq = dpp_u<kDppSwap12>(id), il = dpp_u<kDppShl<4>>(id), ir = dpp_u<kDppShr<4>>(id);
+    const float pt = mid ? tq : (k < 4 ? tl : tr);
+    const uint32_t pi = mid ? iq : (k < 4 ? il : ir);
+    grp_cswap(t, id, pt, pi, true, mid ? (k == 1 || k == 5) : k < 4);
+  }
+  grp_layer_shift<4>(t, id, k == 1 || k == 2 || k == 5 || k == 6, k < 4);  // (1,5)(2,6)
+  grp_layer_shift<3>(t, id, k == 1 || k == 3 || k == 4 || k == 6, k == 1 || k == 3);  // (1,4)(3,6)
+  grp_layer_shift<2>(t, id, k >= 2 && k <= 5, k == 2 || k == 3);  // (2,4)(3,5)
+  grp_layer_shift<1>(t, id, k == 3 || k == 4, k == 3);  // (3,4)
+}
+// Exchange with lane k^4 of the group.
+__device__ __forceinline__ uint32_t grp_xor4_u(uint32_t v, int k) {
+  const uint32_t l = dpp_u<kDppShl<4>>(v), r = dpp_u<kDppShr<4>>(v);
+  return k < 4 ? l : r;
+}
+// Group-wide min of (t, k), ties to the lower k: the first triangle of a leaf
+// with the smallest t, as the reference's strict `>` scan keeps it.
+__device__ __forceinline__ void grp_min_first(float &t, uint32_t &kk, int k) {
+  float pt;
+  uint32_t pk;
+  bool tk;
+  pt = dpp_f<kDppXor1>(t); pk = dpp_u<kDppXor1>(kk);
+  tk = pt < t || (pt == t && pk < kk); t = tk ? pt : t; kk = tk ? pk : kk;
+  pt = dpp_f<kDppXor2>(t); pk = dpp_u<kDppXor2>(kk);
+  tk = pt < t || (pt == t && pk < kk); t = tk ? pt : t; kk = tk ? pk : kk;
+  pt = __uint_as_float(grp_xor4_u(__float_as_uint(t), k)); pk = grp_xor4_u(kk, k);
+  tk = pt < t || (pt == t && pk < kk); t = tk ? pt : t; kk = tk ? pk : kk;
+}
+__device__ __forceinline__ uint32_t grp_or(uint32_t v, int k) {
+  v |= dpp_u<kDppXor1>(v);
+  v |= dpp_u<kDppXor2>(v);
+  v |= grp_xor4_u(v, k);
+  return v;
+}
+
+// mesh_run (non-ANY) executed by an 8-lane group on one ray; S is the same in
+// all 8 lanes and stays so. st = the owner lane's LDS stack column.
+template <int BLOCK, bool FAST>
+__device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear,
+                                              float tFar, LdsStack<BLOCK> st, MState &S, int k) {
+  uint32_t word = S.word, flist = S.flist, fcnt = S.fcnt, fnode = S.fnode, cwnext = S.cwnext, gk = S.gk;
+  float fbest = S.fbest, tnext = S.tnext, gbest = S.gbest;
+  int depth = S.depth;
+  bool have_t = S.have_t;
+  const int gbase = (threadIdx.x & 63) & ~7;
+  for (;;) {
+    if (word != rtl::kInvalidChild) {
+      if (word & rtl::kLeafBit) {
+        const uint32_t first = (word >> 3) & rtl::kMaxLeafFirstTri;
+        const uint32_t n = (word & 7u) + 1u;
+        float tk = kInf;
+        if ((uint32_t)k < n) {
+          const float4 *q = reinterpret_cast<const float4 *>(sc.tris + first + k);
+          tk = tri_t(q[0], q[1], q[2], o, d);
+          if (!(tk < kInf)) tk = kInf;  // a NaN t never wins the strict scan
+        }
+        uint32_t kk = (uint32_t)k;
+        grp_min_first(tk, kk, k);
+        if (tk < kInf) {
+          if (tk < fbest) fbest = tk;
+          if (tk < gbest) { gbest = tk; gk = first + kk; }
+        }
+      } else {
+        const rtl::GNode *nd = sc.nodes + word;
+        const float2 *bp = reinterpret_cast<const float2 *>(nd->box[k]);
+        const float2 b01 = bp[0], b23 = bp[1], b45 = bp[2];
+        const uint32_t cwk = nd->child[k];
+        float t = slab<FAST>(b01.x, b01.y, b23.x, b23.y, b45.x, b45.y, o, inv, tNear, tFar);
+        uint32_t id = (uint32_t)k;
+        grp_sort8(t, id, k);
+        // misses (-1) sort first; the entries to visit are the suffix from i0
+        const uint32_t i0 = (uint32_t)__popcll((__ballot(t < 0.0f) >> gbase) & 0xFFull);
+        const uint32_t c = 8u - i0;
+        const uint32_t l = grp_or(t < 0.0f ? 0u : id << (3u * ((uint32_t)k - i0)), k);
+        const float tf = __shfl(t, gbase + (int)(i0 & 7u), 64);
+        const uint32_t idf = __shfl(id, gbase + (int)(i0 & 7u), 64);
+        const uint32_t cwf = __shfl(cwk, gbase + (int)idf, 64);
+        if (c != 0) {
+          if (depth >= 1) {
+            st.at(depth - 1, 0) = fnode;
+            st.at(depth - 1, 1) = flist | (fcnt << 24);
+            st.at(depth - 1, 2) = __float_as_uint(fbest);
+          }
+          ++depth;
+          fnode = word; flist = l; fcnt = c; fbest = kInf;
+          tnext = tf;
+          cwnext = cwf;
+          have_t = true;
+        }
+      }
+      word = rtl::kInvalidChild;
+    }
+    if (depth == 0) break;
+    if (fcnt == 0) {
+      --depth;
+      if (depth == 0) break;
+      const float child_best = fbest;
+      fnode = st.at(depth - 1, 0);
+      const uint32_t lc = st.at(depth - 1, 1);
+      flist = lc & 0xFFFFFFu;
+      fcnt = lc >> 24;
+      fbest = __uint_as_float(st.at(depth - 1, 2));
+      if (child_best < fbest) fbest = child_best;
+      have_t = false;
+      continue;
+    }
+    const uint32_t j = flist & 7u;
+    flist >>= 3;
+    fcnt -= 1;
+    if (!have_t) {
+      const rtl::GNode *nd = sc.nodes + fnode;
+      const float *b = nd->box[j];
+      cwnext = nd->child[j];
+      tnext = slab<FAST>(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
+    }
+    have_t = false;
+    if (fbest < tnext) { fcnt = 0; continue; }
+    word = cwnext;
+  }
+  S.gk = gk;
+  S.gbest = gbest;
+}
+
+// Primary-ray mesh intersection for a whole wave (every lane of the wave must
+// call it, with active = false for lanes without a pixel): each lane traverses
+// its own ray until at most kCoopRays rays remain, then those finish in 8-lane
+// groups. The result is the same as mesh_trace's, bit for bit.
+template <int BLOCK>
+__device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
+                                                  bool active, uint32_t *stk_block, float &out_t,
+                                                  uint32_t &out_k) {
+  NoCnt cnt;
+  const int lane = threadIdx.x & 63;
+  LdsStack<BLOCK> st{stk_block + threadIdx.x};
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
+  const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+  MState S{rtl::kInvalidChild, 0u, 0u, sc.root, rtl::kInvalidChild, rtl::kInvalidChild, kInf, 0.0f, kInf, 0,
+           false};
+  bool pending = false;
+  if (active && sc.root != rtl::kInvalidChild) {
+    if (sc.root & rtl::kLeafBit) {
+      S.word = sc.root;
+      pending = true;
+    } else {
+      uint32_t l, c, cwf;
+      float tf;
+      const bool entered = fast ? mesh_root<true>(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)
+                                : mesh_root<false>(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt);
+      if (entered) {
+        S.flist = l; S.fcnt = c; S.tnext = tf; S.cwnext = cwf; S.depth = 1; S.have_t = true;
+        pending = true;
+      }
+    }
+  }
+  bool suspended = false;
+  if (pending)
+    suspended = fast ? mesh_run<BLOCK, false, true, true>(sc, o, d, inv, tNear, tFar, st, S, cnt)
+                     : mesh_run<BLOCK, false, false, true>(sc, o, d, inv, tNear, tFar, st, S, cnt);
+  const uint64_t U = __ballot(suspended);  // wave-uniform
+  if (U != 0) {
+    const int g = lane >> 3, k = lane & 7;
+    const int n = __popcll(U);
+    uint64_t m = U;
+    for (int i = 0; i < g && i < n; ++i) m &= m - 1;
+    const int owner = g < n ? (int)__builtin_ctzll(m) : lane;
+    // gather the owner's ray and state (all 64 lanes active here)
+    const f3 go{__shfl(o.x, owner, 64), __shfl(o.y, owner, 64), __shfl(o.z, owner, 64)};
+    const f3 gd{__shfl(d.x, owner, 64), __shfl(d.y, owner, 64), __shfl(d.z, owner, 64)};
+    const f3 ginv{__shfl(inv.x, owner, 64), __shfl(inv.y, owner, 64), __shfl(inv.z, owner, 64)};
+    const float gtf = __shfl(tFar, owner, 64);
+    const bool gfast = __shfl((int)fast, owner, 64) != 0;
+    MState G;
+    G.word = __shfl(S.word, owner, 64);
+    G.flist = __shfl(S.flist, owner, 64);
+    G.fcnt = __shfl(S.fcnt, owner, 64);
+    G.fnode = __shfl(S.fnode, owner, 64);
+    G.cwnext = __shfl(S.cwnext, owner, 64);
+    G.gk = __shfl(S.gk, owner, 64);
+    G.fbest = __shfl(S.fbest, owner, 64);
+    G.tnext = __shfl(S.tnext, owner, 64);
+    G.gbest = __shfl(S.gbest, owner, 64);
+    G.depth = __shfl(S.depth, owner, 64);
+    G.have_t = __shfl((int)S.have_t, owner, 64) != 0;
+    if (g < n) {
+      const LdsStack<BLOCK> gst{stk_block + (threadIdx.x & ~63) + owner};
+      if (gfast)
+        mesh_run_coop<BLOCK, true>(sc, go, gd, ginv, tNear, gtf, gst, G, k);
+      else
+        mesh_run_coop<BLOCK, false>(sc, go, gd, ginv, tNear, gtf, gst, G, k);
+    }
+    // each suspended lane takes the result of its group (group index = rank of its bit)
+    const int mg = __popcll(U & ((1ull << lane) - 1ull));
+    const float rb = __shfl(G.gbest, (mg & 7) * 8, 64);
+    const uint32_t rk = __shfl(G.gk, (mg & 7) * 8, 64);
+    if (suspended) { S.gbest = rb; S.gk = rk; }
+  }
+  out_t = S.gbest;
+  out_k = S.gk;
+  return S.gk != rtl::kInvalidChild;
 }
 
 template <int BLOCK, bool ANY, class CT>
