@@ -5,7 +5,12 @@ Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355
 Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
 1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
 the pure intersection hot path), over a deterministic 64-frame camera orbit
-(SURVEY.md 8(d)). A "step" is one frame. At N=1 the other BASELINE configs
+(SURVEY.md 8(d)). A "step" is one frame. The orbit's frames are independent,
+so --inflight (default 3, triple buffering) of them are in flight at once, each on its own HIP
+stream and framebuffer: the next frame's tiles fill the GPU while the previous
+frame's last tiles (grazing rays at the silhouette, the per-frame tail)
+finish. value = rays of all K frames / wall time of the K frames; the
+one-frame-at-a-time latency is reported beside it ("frame_latency"). At N=1 the other BASELINE configs
 are measured the same way and reported under "extra" (rank 0): the SDF grid
 (configs[2]) on a 256^3 SDF of stanford-bunny generated on the GPU (stand-in:
 example_grid_large.grid is missing from the reference) and on the shipped
@@ -18,16 +23,19 @@ Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every frame is
 split into 16-row bands dealt round-robin to the ranks (load balance: the model
 covers the middle rows); each rank renders its bands packed, then ONE RCCL
 gather per frame brings colour+t (8 B/pixel) to rank 0, which de-interleaves
-them on the device. Gathers are double-buffered so frame k's gather overlaps
-frame k+1's render. Total work per step is fixed (one 1080p frame), so scaling
+them on the device. Frames rotate over max(2, --inflight) streams with their
+own packed buffers, so frame k's gather (and its untile on rank 0) overlaps
+the next frames' renders. Total work per step is fixed (one 1080p frame), so scaling
 is "strong"; value = pixels of all frames / max-over-ranks wall time.
 
 Timing: W untimed warm-up frames, then exactly K frames between barrier +
 torch.cuda.synchronize() on both sides; max over ranks. Inputs are resident
 in HBM before the timed region. Roofline: algorithmic bytes per launch
 (SURVEY.md 8(d) byte model, counted exactly by a diagnostic variant of the
-same kernel over the same frames) / the render kernel's average duration
-(HIP events around each launch on the launch stream); peak 8.0 TB/s HBM.
+same kernel over the same frames) / the render kernel's average launch
+duration (HIP events around each launch on its own stream; what rocprofv3's
+kernel stats report); the amortized rate (wall / K, launches overlap) is
+reported beside it. Peak 8.0 TB/s HBM.
 cpu_baseline: the oracle (C++ restatement of the reference's CPU path, with
 the ISPC kernels in scalar C++) on the host cores, rank 0 at N=1 only.
 """
@@ -65,6 +73,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="orbit frames in flight (one HIP stream each); 1 = one frame at a time")
     ap.add_argument("--dist", action="store_true",
                     help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
@@ -84,32 +94,44 @@ def frame_params(n_frames):
             for k in range(n_frames)]
 
 
-def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG):
-    """N=1: full frames, render kernel only, launched on torch's current stream
-    (the events below are recorded on that same stream). Returns (wall_s,
-    kernel_ms_avg, buffers)."""
+def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG, inflight=2):
+    """N=1: full frames, render kernel only. Frame k is issued on stream
+    k % inflight with its own framebuffer, so up to `inflight` independent
+    frames of the orbit are in flight: the next frame's tiles fill the GPU
+    while the previous frame's last (grazing-ray) tiles finish. inflight=1 is
+    one frame at a time. HIP events bracket each launch on its own stream.
+    Returns (wall_s, kernel_ms_avg, buffers of the last frame)."""
     dev = torch.device("cuda")
-    color = torch.empty((H, W), dtype=torch.int32, device=dev)
-    tbuf = torch.empty((H, W), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream().cuda_stream
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    bufs = [(torch.empty((H, W), dtype=torch.int32, device=dev),
+             torch.empty((H, W), dtype=torch.float32, device=dev)) for _ in range(inflight)]
+
+    def issue(k, ev=None):
+        st = streams[k % inflight]
+        c, t = bufs[k % inflight]
+        with torch.cuda.stream(st):
+            if ev:
+                ev[0].record(st)
+            scene.render_device(params[k], c.data_ptr(), t.data_ptr(), W, H, clear=True,
+                                stream=st.cuda_stream)
+            if ev:
+                ev[1].record(st)
+
     for k in range(warmup):
-        scene.render_device(params[k], color.data_ptr(), tbuf.data_ptr(), W, H, clear=True, stream=stream)
+        issue(k)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        evs[k][0].record()
-        scene.render_device(params[warmup + k], color.data_ptr(), tbuf.data_ptr(), W, H, clear=True,
-                            stream=stream)
-        evs[k][1].record()
+        issue(warmup + k, evs[k])
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kms = sum(a.elapsed_time(b) for a, b in evs) / steps
-    return wall, kms, (color, tbuf)
+    return wall, kms, bufs[(warmup + steps - 1) % inflight]
 
 
-def run_distributed(scene, params, warmup, steps, rank, world, band):
+def run_distributed(scene, params, warmup, steps, rank, world, band, nslots=2):
     """N>1: row bands per rank + one RCCL gather per frame to rank 0.
     With the gloo backend (RTAMD_DIST_BACKEND=gloo: several ranks sharing one
     GPU, for testing the protocol on a 1-GPU box) the packed bands are staged
@@ -120,12 +142,15 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
     per = max(rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(t)) for t in tiles)
     # packed slot: [colour (per) | t (per)] as int32 words, double-buffered; rank 0
     # gathers straight into rank-major rows of one [world, 2*per] buffer per slot
-    bufs = [torch.zeros(2 * per, dtype=torch.int32, device=dev) for _ in range(2)]
-    stacked = ([torch.empty((world, 2 * per), dtype=torch.int32, device=dev) for _ in range(2)]
+    bufs = [torch.zeros(2 * per, dtype=torch.int32, device=dev) for _ in range(nslots)]
+    stacked = ([torch.empty((world, 2 * per), dtype=torch.int32, device=dev) for _ in range(nslots)]
                if rank == 0 else None)
-    recv = [list(stacked[s].unbind(0)) for s in range(2)] if rank == 0 else None
-    frame_c = torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev) if rank == 0 else None
-    frame_t = torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev) if rank == 0 else None
+    recv = [list(stacked[s].unbind(0)) for s in range(nslots)] if rank == 0 else None
+    # rank 0: one untiled frame per slot (the two slots' untiles run on different streams)
+    frame_c = [torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev) for _ in range(nslots)] \
+        if rank == 0 else None
+    frame_t = [torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev) for _ in range(nslots)] \
+        if rank == 0 else None
     tile = tiles[rank]
     ev = []
 
@@ -134,47 +159,54 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
         base = stacked[slot].data_ptr()
         rtamd._lib.check(rtamd.lib().rt_untile_device(
             ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * per), 2 * per,
-            ctypes.c_void_p(frame_c.data_ptr()), ctypes.c_void_p(frame_t.data_ptr()), W_IMG, H_IMG,
+            ctypes.c_void_p(frame_c[slot].data_ptr()), ctypes.c_void_p(frame_t[slot].data_ptr()), W_IMG, H_IMG,
             ctypes.byref(tiles[0]), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+
+    # slot s = frame k % nslots: its own stream, packed buffer and gather target
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslots - 1)]
+
+    def finish(slot):
+        # the slot's previous gather must land before its buffers are reused
+        pending[slot].wait()
+        if rank == 0:
+            untile(slot)
+        pending[slot] = None
 
     def step(k, timed):
         last[0] = k
-        slot = k & 1
+        slot = k % nslots
         b = bufs[slot]
-        if pending[slot] is not None:
-            pending[slot].wait()
-            if rank == 0:
-                untile(slot)
-            pending[slot] = None
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        scene.render_device(params[k], b.data_ptr(), b.data_ptr() + 4 * per, W_IMG, H_IMG,
-                            clear=True, tile=tile, stream=torch.cuda.current_stream().cuda_stream)
-        if timed:
-            e1.record()
-            ev.append((e0, e1))
-        if staged:
-            host = b.cpu()
-            lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
-            dist.gather(host, gather_list=lst, dst=0)
-            if rank == 0:
-                stacked[slot].copy_(torch.stack(lst))
-                untile(slot)
-            return
-        pending[slot] = dist.gather(b, gather_list=recv[slot] if rank == 0 else None, dst=0,
-                                    async_op=True)
+        with torch.cuda.stream(streams[slot]):
+            if pending[slot] is not None:
+                finish(slot)
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            scene.render_device(params[k], b.data_ptr(), b.data_ptr() + 4 * per, W_IMG, H_IMG,
+                                clear=True, tile=tile, stream=streams[slot].cuda_stream)
+            if timed:
+                e1.record()
+                ev.append((e0, e1))
+            if staged:
+                host = b.cpu()
+                lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                dist.gather(host, gather_list=lst, dst=0)
+                if rank == 0:
+                    stacked[slot].copy_(torch.stack(lst))
+                    untile(slot)
+                return
+            pending[slot] = dist.gather(b, gather_list=recv[slot] if rank == 0 else None, dst=0,
+                                        async_op=True)
 
     def drain():
         # oldest first, so the frame left in frame_c/frame_t is the last one rendered
-        for slot in (last[0] + 1) & 1, last[0] & 1:
+        for j in range(nslots - 1, -1, -1):
+            slot = (last[0] - j) % nslots
             if pending[slot] is not None:
-                pending[slot].wait()
-                if rank == 0:
-                    untile(slot)
-                pending[slot] = None
+                with torch.cuda.stream(streams[slot]):
+                    finish(slot)
 
-    pending = [None, None]
+    pending = [None] * nslots
     last = [0]
     for k in range(warmup):
         step(k, False)
@@ -190,19 +222,31 @@ def run_distributed(scene, params, warmup, steps, rank, world, band):
     dist.barrier()
     wall = time.perf_counter() - t0
     kms = sum(a.elapsed_time(b) for a, b in ev) / steps
-    return wall, kms, tile, (frame_c, frame_t)
+    ls = last[0] % nslots
+    return wall, kms, tile, (frame_c[ls], frame_t[ls]) if rank == 0 else (None, None)
 
 
-def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG):
+def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None):
+    """Algorithmic bytes per launch (SURVEY.md 8(d) byte model, counted exactly
+    by the counting variant of the kernel over the same frames) / the kernel's
+    event-timed average launch duration over the timed region (kernel_ms, what
+    rocprofv3's kernel stats report). With frames in flight the launches
+    overlap; the amortized rate (wall / launches) is reported beside it."""
     c = scene.count_work(params, W, H, clear=True, tile=tile)
     npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
     algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params)
     achieved = algo / (kms * 1e-3) / 1e9
     per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
-            "work_per_ray": per_ray}
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
+           "work_per_ray": per_ray}
+    if amortized_ms is not None:
+        # launches overlap (frames in flight): algorithmic bytes per amortized launch.
+        # The byte model counts cache-served bytes, so this can exceed the HBM peak.
+        out["amortized_ms_per_launch"] = round(amortized_ms, 5)
+        out["amortized_achieved"] = round(algo / (amortized_ms * 1e-3) / 1e9, 1)
+    return out
 
 
 def pmc_traffic(workload, W, H, frames=16):
@@ -280,7 +324,7 @@ EXTRAS = [
 ]
 
 
-def run_extras(warmup, steps):
+def run_extras(warmup, steps, inflight):
     out = {}
     for key, src, W, H, desc in EXTRAS:
         if "." in src:
@@ -291,11 +335,11 @@ def run_extras(warmup, steps):
         sc.set_plane(None)
         orbit = WL.orbit_positions(64)
         prm = [WL.params_for(orbit[k % 64], W, H, rtamd.ShadingMode.Normal) for k in range(warmup + steps)]
-        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H)
+        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H, inflight)
         out[key] = {"workload": f"{desc}, {W}x{H} primary rays, same orbit",
                     "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
                     "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
-                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H)}
+                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps)}
         sc.close()
         torch.cuda.synchronize()
     return out
@@ -334,6 +378,10 @@ def cpu_baseline(name, budget_s):
 
 
 def main():
+    # libraries (RCCL, gloo) print banners to stdout: send fd 1 to stderr and
+    # keep the real stdout for the one JSON line
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -366,22 +414,27 @@ def main():
     scene.set_plane(None)
     params = frame_params(a.warmup + a.steps)
 
+    latency = None
     if not use_dist:
-        wall, kms, _ = run_single(scene, params, a.warmup, a.steps)
+        wall, kms, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.inflight)
         tile = None
+        if a.inflight > 1:  # single-frame latency (one frame at a time), reported beside
+            lwall, lkms, _ = run_single(scene, params, min(a.warmup, 8), min(a.steps, 64), inflight=1)
+            latency = {"ms_per_frame": round(lwall * 1e3 / min(a.steps, 64), 4),
+                       "kernel_ms": round(lkms, 5)}
     else:
         wall, kms, tile, frame = run_distributed(scene, params, a.warmup, a.steps, rank, world,
-                                                 a.band_rows)
+                                                 a.band_rows, max(2, a.inflight))
         t = torch.tensor([wall], dtype=torch.float64,
                          device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
         if rank == 0:  # the gathered last frame must equal a whole-frame render of it
-            _, _, (c1, t1) = run_single(scene, params[-1:], 0, 1)
+            _, _, (c1, t1) = run_single(scene, params[-1:], 0, 1, inflight=1)
             check_equal = bool(torch.equal(c1, frame[0]) and torch.equal(t1.view(torch.int32),
                                                                          frame[1].view(torch.int32)))
 
-    rl = roofline(scene, params[a.warmup:], tile, kms)
+    rl = roofline(scene, params[a.warmup:], tile, kms, amortized_ms=wall * 1e3 / a.steps)
     if pmc is not None:
         rl["traffic"] = None if pmc[0] is None else round(pmc[0])
         rl["traffic_detail"] = pmc[1]
@@ -396,18 +449,21 @@ def main():
                                "(BASELINE configs[1]); Normal shading, no plane",
                    "resolution": [W_IMG, H_IMG], "camera": "orbit r=2.5 h=0.5 fovy 45",
                    "parallelism": f"row bands of {a.band_rows} rows x {world} GPUs + RCCL gather"
-                   if use_dist else "1 GPU, 1 thread per pixel"},
+                   if use_dist else "1 GPU, 1 thread per pixel",
+                   "frames_in_flight": a.inflight},
         "roofline": rl,
     }
+    if latency is not None:
+        out["frame_latency"] = latency
     if use_dist and rank == 0:
         out["frame_check"] = {"gathered_equals_single_render": check_equal,
                               "backend": dist.get_backend()}
     if rank == 0 and not use_dist and not a.no_extra:
-        out["extra"] = run_extras(min(a.warmup, 8), min(a.steps, 64))
+        out["extra"] = run_extras(min(a.warmup, 8), min(a.steps, 64), a.inflight)
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()

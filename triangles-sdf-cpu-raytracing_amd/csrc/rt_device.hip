@@ -482,6 +482,7 @@ struct rt_scene {
   uint32_t sched_grid = 0;
   bool sched_on = true;
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
+  hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
 };
 
@@ -557,7 +558,14 @@ void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool 
 int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
   fa.order = nullptr;
   fa.cost = nullptr;
-  if (!s->sched_on) return RT_OK;
+  // Frames of this scene arriving on alternating streams are frames in flight:
+  // each one's tail is filled by the next frame's tiles, and an order_kernel
+  // between a stream's frames would serialise them (it needs a whole CU, which
+  // frees only when the other stream's frame drains). Such frames render in
+  // blockIdx order and leave the schedule state alone.
+  const bool same_stream = stream == s->last_stream;
+  s->last_stream = stream;
+  if (!s->sched_on || !same_stream) return RT_OK;
   const uint32_t nb = gx * gy;
   if (nb > s->sched_cap) {
     if (s->d_cost) (void)hipFree(s->d_cost);
