@@ -225,3 +225,48 @@ def test_schedule_state_is_output_neutral(gpu):
             assert np.array_equal(outs[(rep, k)][0], outs[(0, k)][0])
         if k < 3:
             assert_same(S.ref_frame(name, W, H, "primary", pos), outs[(1, k)], f"schedule frame {k}")
+
+
+SORT8_PAIRS = [(0, 1), (2, 3), (4, 5), (6, 7), (0, 2), (1, 3), (4, 6), (5, 7), (1, 2), (5, 6),
+               (0, 4), (3, 7), (1, 5), (2, 6), (1, 4), (3, 6), (2, 4), (3, 5), (3, 4)]
+
+
+def test_group_primitives_match_scalar_forms(gpu):
+    """The cooperative tail's 8-lane primitives (DPP exchanges) equal the scalar
+    forms: the sort8 network (raytracing.hpp:188-213) including its tie order,
+    the first-wins min of a leaf scan, and the OR reduction."""
+    import ctypes as C
+
+    from rtamd._lib import check, lib
+    rng = np.random.default_rng(9)
+    n = 4000
+    keys = rng.choice(np.array([-1.0, 0.5, 0.5, 1.0, 2.0, 2.0, 3.0, np.inf], np.float32), size=(n, 8))
+    keys[: n // 2] = rng.normal(size=(n // 2, 8)).astype(np.float32)
+    keys[: n // 4, ::3] = -1.0
+    keys = np.ascontiguousarray(keys, np.float32)
+    st = np.zeros((n, 8), np.float32)
+    sid = np.zeros((n, 8), np.uint32)
+    mt = np.zeros(n, np.float32)
+    mk = np.zeros(n, np.uint32)
+    orv = np.zeros(n, np.uint32)
+    L = lib()
+    L.rtx_grp_test.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 5
+    check(L.rtx_grp_test(keys.ctypes.data, n, st.ctypes.data, sid.ctypes.data, mt.ctypes.data,
+                         mk.ctypes.data, orv.ctypes.data))
+    for g in range(n):
+        t = list(keys[g])
+        ids = list(range(8))
+        for a, b in SORT8_PAIRS:
+            if t[a] > t[b]:
+                t[a], t[b] = t[b], t[a]
+                ids[a], ids[b] = ids[b], ids[a]
+        assert st[g].tolist() == [float(x) for x in t] and sid[g].tolist() == ids, (g, keys[g])
+        lt, lk = np.float32(np.inf), 8
+        for k in range(8):
+            if lt > keys[g, k]:
+                lt, lk = keys[g, k], k
+        if lk < 8:
+            assert mt[g] == lt and mk[g] == lk, (g, keys[g], mt[g], mk[g])
+        else:
+            assert mt[g] == np.inf
+    assert np.all(orv == 0o11111111)

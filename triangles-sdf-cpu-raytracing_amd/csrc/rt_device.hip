@@ -445,6 +445,40 @@ __global__ __launch_bounds__(1024) void order_kernel(uint32_t *cost, uint32_t *o
   }
 }
 
+// Diagnostic: the world-space primary ray of every pixel, as render_kernel
+// computes it (image row yo, loop row y = H - yo - 1).
+__global__ void eye_rays_kernel(rt_render_params P, int W, int H, float *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * H) return;
+  const int yo = i / W, x = i - yo * W;
+  const f3 d = eye_ray(x, H - yo - 1, W, H, P.proj_inv, P.view_inv);
+  out[3 * i] = d.x;
+  out[3 * i + 1] = d.y;
+  out[3 * i + 2] = d.z;
+}
+
+// Diagnostic: the 8-lane group primitives of the cooperative tail on test
+// vectors (one 8-lane group per vector of 8 keys): sort8 across lanes, the
+// first-wins min, the OR reduction. Checked against the scalar forms in tests.
+__global__ void grp_test_kernel(const float *keys, int n, float *st, uint32_t *sid, float *mt,
+                                uint32_t *mk, uint32_t *orv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // blockDim = 64: 8 groups per wave
+  const int g = i >> 3, k = i & 7;
+  const bool ok = g < n;
+  float t = ok ? keys[8 * g + k] : 0.0f;
+  uint32_t id = (uint32_t)k;
+  grp_sort8(t, id, k);
+  float m = ok ? keys[8 * g + k] : 0.0f;
+  uint32_t kk = (uint32_t)k;
+  grp_min_first(m, kk, k);
+  const uint32_t o = grp_or(1u << (3 * k), k);
+  if (ok) {
+    st[8 * g + k] = t;
+    sid[8 * g + k] = id;
+    if (k == 0) { mt[g] = m; mk[g] = kk; orv[g] = o; }
+  }
+}
+
 }  // namespace
 
 // ================================================================== C ABI ==
@@ -481,6 +515,7 @@ struct rt_scene {
   uint32_t sched_cap = 0;
   uint32_t sched_grid = 0;
   bool sched_on = true;
+  bool coop = true;  // mesh primary rays: cooperative tail (rtx_set_coop)
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
@@ -495,7 +530,7 @@ GridDev grid_dev(const rt_scene *s) {
 }
 
 MeshDev mesh_dev(const rt_scene *s) {
-  MeshDev m{s->d_nodes, s->d_tris, s->root, {}};
+  MeshDev m{s->d_nodes, s->d_tris, s->root, {}, s->coop};
   for (int k = 0; k < 6; ++k) m.rbox[k] = s->root_box[k];
   return m;
 }
@@ -1076,6 +1111,53 @@ int rtx_wave_stamps(rt_scene *s, const rt_render_params *params, int32_t W, int3
   if (rc) return rc;
   if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
   *nwaves = nw;
+  return RT_OK;
+}
+
+// Diagnostic: primary ray directions as the render kernel computes them (host buffer [H][W][3]).
+int rtx_eye_rays(const rt_render_params *p, int32_t W, int32_t H, float *out) {
+  int rc = check_params(p, W, H);
+  if (rc) return rc;
+  float *d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)W * H * 12));
+  eye_rays_kernel<<<(W * H + 255) / 256, 256>>>(*p, W, H, d);
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)W * H * 12, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
+  return RT_OK;
+}
+
+// Diagnostic: run the 8-lane group primitives on n vectors of 8 keys (host buffers).
+int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *mt, uint32_t *mk,
+                 uint32_t *orv) {
+  if (n <= 0) return set_err(RT_E_INVALID, "n must be positive");
+  float *dk = nullptr, *dst = nullptr, *dmt = nullptr;
+  uint32_t *dsid = nullptr, *dmk = nullptr, *dor = nullptr;
+  const size_t n8 = (size_t)n * 8;
+  HIP_TRY(hipMalloc(&dk, n8 * 4));
+  HIP_TRY(hipMalloc(&dst, n8 * 4));
+  HIP_TRY(hipMalloc(&dsid, n8 * 4));
+  HIP_TRY(hipMalloc(&dmt, (size_t)n * 4));
+  HIP_TRY(hipMalloc(&dmk, (size_t)n * 4));
+  HIP_TRY(hipMalloc(&dor, (size_t)n * 4));
+  HIP_TRY(hipMemcpy(dk, keys, n8 * 4, hipMemcpyHostToDevice));
+  grp_test_kernel<<<(unsigned)((n8 + 63) / 64), 64>>>(dk, n, dst, dsid, dmt, dmk, dor);
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(st, dst, n8 * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(sid, dsid, n8 * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(mt, dmt, (size_t)n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(mk, dmk, (size_t)n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(orv, dor, (size_t)n * 4, hipMemcpyDeviceToHost);
+  for (void *q : {(void *)dk, (void *)dst, (void *)dsid, (void *)dmt, (void *)dmk, (void *)dor}) (void)hipFree(q);
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
+  return RT_OK;
+}
+
+// Diagnostic A/B switch: cooperative tail of the mesh primary path on (default) / off.
+int rtx_set_coop(rt_scene *s, int on) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  s->coop = on != 0;
   return RT_OK;
 }
 

@@ -56,6 +56,7 @@ struct MeshDev {
   // monotone in the box bounds when 1/d is finite), so the root node need not
   // be fetched. Used only when all three 1/d components are finite.
   float rbox[6];
+  bool coop;  // primary rays: cooperative tail enabled (diagnostic switch rtx_set_coop)
 };
 
 // triangle_intersection (ray_pack.ispc:132-165) on one triangle already in
@@ -507,14 +508,26 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
     }
   }
   bool suspended = false;
-  if (pending)
+  if (pending && sc.coop)
     suspended = fast ? mesh_run<BLOCK, false, true, true>(sc, o, d, inv, tNear, tFar, st, S, cnt)
                      : mesh_run<BLOCK, false, false, true>(sc, o, d, inv, tNear, tFar, st, S, cnt);
-  const uint64_t U = __ballot(suspended);  // wave-uniform
-  if (U != 0) {
+  else if (pending)
+    (void)(fast ? mesh_run<BLOCK, false, true, false>(sc, o, d, inv, tNear, tFar, st, S, cnt)
+                : mesh_run<BLOCK, false, false, false>(sc, o, d, inv, tNear, tFar, st, S, cnt));
+  // Rays still traversing: at most kCoopRays per branch of the fast/exact
+  // dispatch above (each branch suspends on its own lane count), so up to
+  // 2 * kCoopRays; they are finished kCoopRays at a time.
+  uint64_t U = __ballot(suspended);  // wave-uniform
+  while (U != 0) {
+    uint64_t R = 0, rest = U;  // the lowest kCoopRays rays of U
+    for (int i = 0; i < kCoopRays && rest != 0; ++i) {
+      R |= rest & (~rest + 1ull);
+      rest &= rest - 1ull;
+    }
+    U &= ~R;
     const int g = lane >> 3, k = lane & 7;
-    const int n = __popcll(U);
-    uint64_t m = U;
+    const int n = __popcll(R);
+    uint64_t m = R;
     for (int i = 0; i < g && i < n; ++i) m &= m - 1;
     const int owner = g < n ? (int)__builtin_ctzll(m) : lane;
     // gather the owner's ray and state (all 64 lanes active here)
@@ -542,11 +555,11 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
       else
         mesh_run_coop<BLOCK, false>(sc, go, gd, ginv, tNear, gtf, gst, G, k);
     }
-    // each suspended lane takes the result of its group (group index = rank of its bit)
-    const int mg = __popcll(U & ((1ull << lane) - 1ull));
+    // each ray of this round takes the result of its group (group = rank of its bit in R)
+    const int mg = __popcll(R & ((1ull << lane) - 1ull));
     const float rb = __shfl(G.gbest, (mg & 7) * 8, 64);
     const uint32_t rk = __shfl(G.gk, (mg & 7) * 8, 64);
-    if (suspended) { S.gbest = rb; S.gk = rk; }
+    if ((R >> lane) & 1ull) { S.gbest = rb; S.gk = rk; }
   }
   out_t = S.gbest;
   out_k = S.gk;
