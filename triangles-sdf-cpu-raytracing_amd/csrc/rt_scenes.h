@@ -847,6 +847,7 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
 // only 3 distinct bounds per axis (min, centre, max: centre + diff == max and
 // min + diff == centre exactly), so the 24 slab distances of the reference
 // are 9 distinct values, computed once each with the reference's operations.
+template <bool FAST>
 __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar,
                                            uint32_t &list, uint32_t &cnt) {
   const f3 center{(bmin.x + bmax.x) / 2.0f, (bmin.y + bmax.y) / 2.0f, (bmin.z + bmax.z) / 2.0f};
@@ -856,18 +857,21 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
   const float y0 = (bmin.y - o.y) * inv.y, y1 = (center.y - o.y) * inv.y, y2 = (hi.y - o.y) * inv.y;
   const float z0 = (bmin.z - o.z) * inv.z, z1 = (center.z - o.z) * inv.z, z2 = (hi.z - o.z) * inv.z;
   // per axis and half: (min, max) of the two slab distances, ISPC operand order
-  const float mnx[2] = {isp_min(x0, x1), isp_min(x1, x2)}, mxx[2] = {isp_max(x0, x1), isp_max(x1, x2)};
-  const float mny[2] = {isp_min(y0, y1), isp_min(y1, y2)}, mxy[2] = {isp_max(y0, y1), isp_max(y1, y2)};
-  const float mnz[2] = {isp_min(z0, z1), isp_min(z1, z2)}, mxz[2] = {isp_max(z0, z1), isp_max(z1, z2)};
+  // FAST (1/d finite, so no NaN operand): IEEE min/max equal ISPC's forms (see slab_fast)
+  auto mn = [](float a, float b) { return FAST ? __builtin_fminf(a, b) : isp_min(a, b); };
+  auto mx = [](float a, float b) { return FAST ? __builtin_fmaxf(a, b) : isp_max(a, b); };
+  const float mnx[2] = {mn(x0, x1), mn(x1, x2)}, mxx[2] = {mx(x0, x1), mx(x1, x2)};
+  const float mny[2] = {mn(y0, y1), mn(y1, y2)}, mxy[2] = {mx(y0, y1), mx(y1, y2)};
+  const float mnz[2] = {mn(z0, z1), mn(z1, z2)}, mxz[2] = {mx(z0, z1), mx(z1, z2)};
   float t[8];
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int x = c >> 2, y = (c & 3) >> 1, z = c & 1;
-    float tMin = isp_max(mnx[x], isp_max(mny[y], mnz[z]));
-    float tMax = isp_min(mxx[x], isp_min(mxy[y], mxz[z]));
-    tMin = isp_max(tMin, tNear);
-    tMax = isp_min(tMax, tFar);
+    float tMin = mx(mnx[x], mx(mny[y], mnz[z]));
+    float tMax = mn(mxx[x], mn(mxy[y], mxz[z]));
+    tMin = mx(tMin, tNear);
+    tMax = mn(tMax, tFar);
     t[c] = (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
     id[c] = (uint32_t)c;
   }
@@ -883,11 +887,10 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
   }
 }
 
-template <int BLOCK, bool NEED_NORMAL, class CT>
-__device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                          LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
-                                          uint32_t &out_node, CT &cnt) {
-  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+template <int BLOCK, bool NEED_NORMAL, bool FAST, class CT>
+__device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear,
+                                            float tFar, LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
+                                            uint32_t &out_node, CT &cnt) {
   const uint32_t root = sc.child[0];
   cnt.add(C_OCT_NODE, 1);
   if (root == 0 || root == rtl::kOctNeverHits) {
@@ -897,21 +900,23 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
     return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d,
                                  inv, tNear, tFar, out_t, out_n, cnt);
   }
-  // top frame: node whose children are being visited, its coords and list
-  uint32_t fnode = 0, flist, fcnt;
+  // top frame: the children block (childrenOffset) of the node whose children
+  // are being visited, its coords and list; frames keep the block, not the
+  // node, so visiting a child costs one dependent load (its word), not two
+  uint32_t fbase = root, flist, fcnt;
   uint32_t ix = 0, iy = 0, iz = 0;
   int depth = 0;  // depth of fnode (root = 0); frames below the top live in LDS
   {
     f3 bmin, bmax;
     float inv_s;
     oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
-    oct_expand(bmin, bmax, o, inv, tNear, tFar, flist, fcnt);
+    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, flist, fcnt);
   }
   for (;;) {
     if (fcnt == 0) {
       if (depth == 0) return false;
       --depth;
-      fnode = st.at(depth, 0);
+      fbase = st.at(depth, 0);
       const uint32_t lc = st.at(depth, 1);
       flist = lc & 0xFFFFFFu;
       fcnt = lc >> 24;
@@ -921,7 +926,7 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
     const uint32_t j = flist & 7u;
     flist >>= 3;
     fcnt -= 1;
-    const uint32_t cn = sc.child[fnode] + j;
+    const uint32_t cn = fbase + j;
     const uint32_t cx = (ix << 1) | (j >> 2), cy = (iy << 1) | ((j >> 1) & 1u), cz = (iz << 1) | (j & 1u);
     const uint32_t cw = sc.child[cn];
     cnt.add(C_OCT_NODE, 1);
@@ -939,14 +944,24 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
       continue;
     }
     uint32_t l, c;
-    oct_expand(bmin, bmax, o, inv, tNear, tFar, l, c);
+    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
     if (c == 0) continue;
-    st.at(depth, 0) = fnode;
+    st.at(depth, 0) = fbase;
     st.at(depth, 1) = flist | (fcnt << 24);
     ++depth;
-    fnode = cn; flist = l; fcnt = c;
+    fbase = cw; flist = l; fcnt = c;
     ix = cx; iy = cy; iz = cz;
   }
+}
+
+template <int BLOCK, bool NEED_NORMAL, class CT>
+__device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
+                                          LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
+                                          uint32_t &out_node, CT &cnt) {
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z))
+    return oct_trace_t<BLOCK, NEED_NORMAL, true>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
+  return oct_trace_t<BLOCK, NEED_NORMAL, false>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
 }
 
 template <int BLOCK, class CT>
