@@ -493,7 +493,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     out.max_depth = std::max(out.max_depth, depth_of[i]);
     for (int c = 0; c < 8; ++c) {
       if ((uint32_t)c < n.nchild) {
-        for (int k = 0; k < 3; ++k) { g.box[c][k] = n.box[c].mn[k]; g.box[c][3 + k] = n.box[c].mx[k]; }
+        for (int k = 0; k < 3; ++k) { g.box[c][2 * k] = n.box[c].mn[k]; g.box[c][2 * k + 1] = n.box[c].mx[k]; }
         const HNode &ch = H[n.child[c]];
         g.child[c] = ch.leaf ? leaf_word(ch) : (uint32_t)gpu_id[n.child[c]];
       } else {

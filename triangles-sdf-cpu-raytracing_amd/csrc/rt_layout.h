@@ -8,9 +8,11 @@
 //  * GNode: one BVH8 INNER node (triangles_raytracing.hpp:10-36). The reference
 //    node is Box8 SoA (192 B) + realCount + offset, with leaves as separate
 //    nodes. Here a node carries its 8 child boxes in AoS order (child c at
-//    box[6c..6c+5]: xMin yMin zMin xMax yMax zMax, the same floats as the
-//    reference Box8) and 8 child WORDS; a leaf child is referenced directly by
-//    its triangle range, so leaves cost no node fetch. Unused slots
+//    box[c][0..5]: xMin xMax yMin yMax zMin zMax -- the same floats as the
+//    reference Box8, the min/max of an axis adjacent so a slab pair is one
+//    64-bit register pair for the packed-math unit) and 8 child WORDS; a
+//    leaf child is referenced directly by its triangle range, so leaves cost
+//    no node fetch. Unused slots
 //    (c >= realCount) hold +inf boxes: under the ISPC slab formula
 //    (ray_pack.ispc:241-273) such a box always yields -1 (miss), so the kernel
 //    may compute or skip them identically. 224 B = 7 x 32 B.

@@ -64,10 +64,14 @@ __device__ __forceinline__ float slab_ispc(float bx0, float by0, float bz0, floa
 // IEEE min/max (signed zeros aside, and a zero entry distance is only ever
 // compared, never used arithmetically), and min/max are associative, so the
 // hardware's 2- and 3-operand v_min/v_max give the same bits in fewer ops.
+typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float slab_fast(float bx0, float by0, float bz0, float bx1, float by1,
                                            float bz1, f3 o, f3 inv, float tNear, float tFar) {
-  const float t1x = (bx0 - o.x) * inv.x, t1y = (by0 - o.y) * inv.y, t1z = (bz0 - o.z) * inv.z;
-  const float t2x = (bx1 - o.x) * inv.x, t2y = (by1 - o.y) * inv.y, t2z = (bz1 - o.z) * inv.z;
+  // (lo, hi) pairs through the packed-math unit: the same IEEE sub and mul per element
+  const v2f tx = (v2f{bx0, bx1} - v2f{o.x, o.x}) * v2f{inv.x, inv.x};
+  const v2f ty = (v2f{by0, by1} - v2f{o.y, o.y}) * v2f{inv.y, inv.y};
+  const v2f tz = (v2f{bz0, bz1} - v2f{o.z, o.z}) * v2f{inv.z, inv.z};
+  const float t1x = tx.x, t2x = tx.y, t1y = ty.x, t2y = ty.y, t1z = tz.x, t2z = tz.y;
   const float tMin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)),
                                      __builtin_fmaxf(__builtin_fminf(t1z, t2z), tNear));
   const float tMax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)),

@@ -134,8 +134,8 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    t[c] = slab<FAST>(bx[6 * c], bx[6 * c + 1], bx[6 * c + 2], bx[6 * c + 3], bx[6 * c + 4],
-                     bx[6 * c + 5], o, inv, tNear, tFar);
+    t[c] = slab<FAST>(bx[6 * c], bx[6 * c + 2], bx[6 * c + 4], bx[6 * c + 1], bx[6 * c + 3],
+                      bx[6 * c + 5], o, inv, tNear, tFar);  // box: xMin xMax yMin yMax zMin zMax
     id[c] = (uint32_t)c;
   }
   sort8(t, id);
@@ -280,7 +280,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       const rtl::GNode *nd = sc.nodes + fnode;
       const float *b = nd->box[j];
       cwnext = nd->child[j];
-      tnext = slab<FAST>(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
+      tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
     }
     have_t = false;
     if (fbest < tnext) { fcnt = 0; continue; }  // pruned; later siblings have larger t
@@ -418,9 +418,9 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
       } else {
         const rtl::GNode *nd = sc.nodes + word;
         const float2 *bp = reinterpret_cast<const float2 *>(nd->box[k]);
-        const float2 b01 = bp[0], b23 = bp[1], b45 = bp[2];
+        const float2 bxx = bp[0], byy = bp[1], bzz = bp[2];  // (min, max) per axis
         const uint32_t cwk = nd->child[k];
-        float t = slab<FAST>(b01.x, b01.y, b23.x, b23.y, b45.x, b45.y, o, inv, tNear, tFar);
+        float t = slab<FAST>(bxx.x, byy.x, bzz.x, bxx.y, byy.y, bzz.y, o, inv, tNear, tFar);
         uint32_t id = (uint32_t)k;
         grp_sort8(t, id, k);
         // misses (-1) sort first; the entries to visit are the suffix from i0
@@ -466,7 +466,7 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
       const rtl::GNode *nd = sc.nodes + fnode;
       const float *b = nd->box[j];
       cwnext = nd->child[j];
-      tnext = slab<FAST>(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, tNear, tFar);
+      tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
     }
     have_t = false;
     if (fbest < tnext) { fcnt = 0; continue; }

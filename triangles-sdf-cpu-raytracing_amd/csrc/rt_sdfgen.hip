@@ -86,10 +86,11 @@ __device__ __forceinline__ f3 closest_on_tri(f3 p, f3 a, f3 b, f3 c, int &feat) 
   return a + ab * v + ac * w;
 }
 
+// bx: xMin xMax yMin yMax zMin zMax (rt_layout.h GNode)
 __device__ __forceinline__ float box_d2(const float *bx, f3 p) {
-  const float dx = fmaxf(fmaxf(bx[0] - p.x, p.x - bx[3]), 0.0f);
-  const float dy = fmaxf(fmaxf(bx[1] - p.y, p.y - bx[4]), 0.0f);
-  const float dz = fmaxf(fmaxf(bx[2] - p.z, p.z - bx[5]), 0.0f);
+  const float dx = fmaxf(fmaxf(bx[0] - p.x, p.x - bx[1]), 0.0f);
+  const float dy = fmaxf(fmaxf(bx[2] - p.y, p.y - bx[3]), 0.0f);
+  const float dz = fmaxf(fmaxf(bx[4] - p.z, p.z - bx[5]), 0.0f);
   return dx * dx + dy * dy + dz * dz;
 }
 
