@@ -206,6 +206,33 @@ int rt_sdf_mesh_destroy(rt_sdf_mesh *m);
 int rt_mesh_subdivide(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, int32_t levels,
                       float *out_vpos4, int64_t *out_nverts, uint32_t *out_idx, int64_t *out_nidx);
 
+/* ---- the viewer's orbit camera and image output --
+ * Camera (src/camera.hpp:7-61, src/camera.cpp:1-72, src/quaternion.hpp:8-70):
+ * position/target plus an orientation quaternion; rotate(dx, dy) is the
+ * viewer's mouse drag (main.cpp:277-280: rotate(-dx, -dy)), zoom(wheel) its
+ * mouse wheel (main.cpp:281-288). Host-only; the state is a plain struct. */
+typedef struct rt_camera_state {
+  float position[3];
+  float target[3];
+  float orientation[4]; /* x, y, z, w (un-normalised after construction, as the reference) */
+  float sensitivity;    /* 0.01 (camera.hpp:55) */
+  int32_t lock_up;
+  float locked_up[3];
+} rt_camera_state;
+int rt_camera_init(const float pos[3], const float target[3], const float up[3], rt_camera_state *c);
+int rt_camera_rotate(rt_camera_state *c, float dx, float dy);
+int rt_camera_reset_position(rt_camera_state *c, const float pos[3]);
+int rt_camera_reset_target(rt_camera_state *c, const float target[3]);
+int rt_camera_set_lock_up(rt_camera_state *c, int on);
+int rt_camera_zoom(rt_camera_state *c, float wheel);
+/* up(), right(), forward() (camera.hpp:29-37); any pointer may be NULL. */
+int rt_camera_basis(const rt_camera_state *c, float up[3], float right[3], float forward[3]);
+/* inverse4x4(lookAtMatrix()) -- the view_inv of rt_render_params. */
+int rt_camera_view_inverse(const rt_camera_state *c, float view_inv[16]);
+/* Write a colour buffer (W*H packed RGBA8, R in the low byte, row 0 = top) as
+ * an 8-bit RGBA PNG (what the viewer shows, main.cpp:239-242). */
+int rt_write_png(const char *path, const uint32_t *color, int32_t W, int32_t H);
+
 #ifdef __cplusplus
 }
 #endif

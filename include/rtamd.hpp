@@ -91,28 +91,43 @@ struct FrameBuffer {
   }
   uint32_t width() const { return w; }
   uint32_t height() const { return h; }
+  // the colour buffer as an 8-bit RGBA PNG
+  void savePNG(const std::string &path) const {
+    check(rt_write_png(path.c_str(), color.data(), (int32_t)w, (int32_t)h));
+  }
 };
 
-// Camera (camera.hpp:7-61): position / target / up; the view matrix is the
-// reference's lookAt of its quaternion-derived up vector.
+// Camera (camera.hpp:7-61, camera.cpp:1-72): the viewer's orbit camera over
+// rt_camera_state -- the reference's quaternion math, bit for bit.
 class Camera {
  public:
-  Camera() = default;
-  Camera(float3 position, float3 target, float3 up = {0.0f, 1.0f, 0.0f})
-      : pos_(position), target_(target), up_(up) {}
-  float3 position() const { return pos_; }
-  float3 target() const { return target_; }
+  Camera() : Camera(float3{0.0f, 0.0f, 2.5f}, float3{}) {}
+  Camera(float3 position, float3 target, float3 up = {0.0f, 1.0f, 0.0f}) {
+    check(rt_camera_init(&position.x, &target.x, &up.x, &s_));
+  }
+  float3 position() const { return {s_.position[0], s_.position[1], s_.position[2]}; }
+  float3 target() const { return {s_.target[0], s_.target[1], s_.target[2]}; }
+  float3 up() const { float3 u, r, f; basis(u, r, f); return u; }
+  float3 right() const { float3 u, r, f; basis(u, r, f); return r; }
+  float3 forward() const { float3 u, r, f; basis(u, r, f); return f; }
+  float sensetivity() const { return s_.sensitivity; }  // (sic) camera.hpp:38
+  void rotate(float dx, float dy) { check(rt_camera_rotate(&s_, dx, dy)); }
+  void resetPosition(float3 p) { check(rt_camera_reset_position(&s_, &p.x)); }
+  void resetTarget(float3 t) { check(rt_camera_reset_target(&s_, &t.x)); }
+  void setLockUp(bool on) { check(rt_camera_set_lock_up(&s_, on ? 1 : 0)); }
+  bool isLockedUp() const { return s_.lock_up != 0; }
+  void zoom(float wheel) { check(rt_camera_zoom(&s_, wheel)); }  // the viewer's mouse wheel
   // inverse4x4(lookAtMatrix())
   float4x4 viewInverse() const {
-    float4x4 vi{}, pi{};
-    const float p[3] = {pos_.x, pos_.y, pos_.z}, t[3] = {target_.x, target_.y, target_.z},
-                u[3] = {up_.x, up_.y, up_.z};
-    check(rt_camera(p, t, u, 45.0f, 1.0f, 0.01f, 100.0f, vi.data(), pi.data()));
+    float4x4 vi{};
+    check(rt_camera_view_inverse(&s_, vi.data()));
     return vi;
   }
+  const rt_camera_state &state() const { return s_; }
 
  private:
-  float3 pos_{0.0f, 0.0f, 2.5f}, target_{}, up_{0.0f, 1.0f, 0.0f};
+  void basis(float3 &u, float3 &r, float3 &f) const { check(rt_camera_basis(&s_, &u.x, &r.x, &f.x)); }
+  rt_camera_state s_{};
 };
 
 // inverse4x4(perspectiveMatrix(fovy, aspect, zNear, zFar)) (main.cpp:198-201)

@@ -234,7 +234,52 @@ struct Camera {
     // camera.cpp:61: normalize(m_orientation) -- result discarded, q stays un-normalized.
   }
   float3 up() const { return normalize(rotateVector({0.0f, 1.0f, 0.0f}, q)); }  // camera.hpp:29-31
+  float3 right() const { return normalize(rotateVector({1.0f, 0.0f, 0.0f}, q)); }  // camera.hpp:32-34
+  float3 forward() const { return normalize(target - pos); }                      // camera.hpp:35-37
   float4x4 lookAtMatrix() const { return lookAt(pos, target, up()); }          // camera.hpp:24-26
+  // ---- the viewer's interaction (camera.cpp:5-72, camera.hpp:39-47) ----
+  float sens = 0.01f;
+  bool lockUp = false;
+  float3 lockedUp{0.0f, 0.0f, 0.0f};
+  Camera() = default;
+  void updateOrientation(float3 up_) {  // camera.cpp:36-62
+    Camera c(pos, target, up_);
+    q = c.q;
+  }
+  static Quat angleAxis(float angle, float3 axis) {  // quaternion.hpp:54-70
+    float3 n = normalize(axis);
+    float half = angle * 0.5f;
+    Quat r;
+    r.w = std::cos(half);
+    r.x = n.x * std::sin(half);
+    r.y = n.y * std::sin(half);
+    r.z = n.z * std::sin(half);
+    return r;
+  }
+  void rotate(float dx, float dy) {  // camera.cpp:5-20
+    float pitch = dy * sens, yaw = dx * sens;
+    Quat qYaw = angleAxis(yaw, up());
+    Quat qPitch = angleAxis(pitch, right());
+    Quat m = qmul(qmul(qPitch, qYaw), q);
+    float n = std::sqrt(m.x * m.x + m.y * m.y + m.z * m.z + m.w * m.w);  // Quaternion::normalized
+    q = {m.x / n, m.y / n, m.z / n, m.w / n};
+    // updateVectors (camera.cpp:22-28)
+    float3 f = normalize(rotateVector({0.0f, 0.0f, -1.0f}, q));
+    float distance = length(target - pos);
+    pos = target - f * distance;
+    if (lockUp) updateOrientation(lockedUp);
+  }
+  void resetPosition(float3 p) { float3 u = up(); pos = p; updateOrientation(u); }    // camera.cpp:64-67
+  void resetTarget(float3 t) { float3 u = up(); target = t; updateOrientation(u); }   // camera.cpp:69-72
+  void setLockUp(bool to) {                                                           // camera.hpp:39-44
+    if (!lockUp && to) lockedUp = up();
+    lockUp = to;
+  }
+  void zoom(float wheel) {  // main.cpp:281-288
+    float distance = length(target - pos);
+    float r = wheel * distance / 25.0f;
+    resetPosition(pos + forward() * r);
+  }
 };
 
 // ------------------------------------------------------------ HitInfo etc --
@@ -1333,4 +1378,49 @@ int cpuref_sdf_points(const float *vpos4, int64_t nverts, const uint32_t *idx, i
   return 0;
 }
 
+
+// Orbit camera (camera.cpp) over a state of 18 floats laid out as
+// rt_camera_state: position[3] target[3] q[4] sensitivity lock_up(int) locked[3].
+static Camera cam_from(const float *st) {
+  Camera c;
+  c.pos = float3(st[0], st[1], st[2]);
+  c.target = float3(st[3], st[4], st[5]);
+  c.q = {st[6], st[7], st[8], st[9]};
+  c.sens = st[10];
+  int32_t lk;
+  std::memcpy(&lk, st + 11, 4);
+  c.lockUp = lk != 0;
+  c.lockedUp = float3(st[12], st[13], st[14]);
+  return c;
+}
+static void cam_to(const Camera &c, float *st) {
+  st[0] = c.pos.x; st[1] = c.pos.y; st[2] = c.pos.z;
+  st[3] = c.target.x; st[4] = c.target.y; st[5] = c.target.z;
+  st[6] = c.q.x; st[7] = c.q.y; st[8] = c.q.z; st[9] = c.q.w;
+  st[10] = c.sens;
+  int32_t lk = c.lockUp ? 1 : 0;
+  std::memcpy(st + 11, &lk, 4);
+  st[12] = c.lockedUp.x; st[13] = c.lockedUp.y; st[14] = c.lockedUp.z;
+}
+// op: 0 init(a=pos, b=target, c3=up) 1 rotate(x, y) 2 resetPosition(a) 3 resetTarget(a)
+//     4 setLockUp(x != 0) 5 zoom(x); view_inv (16 floats) returned after the op.
+void cpuref_cam_op(float *st, int op, const float *a, const float *b, const float *c3, float x, float y,
+                   float *view_inv) {
+  Camera c;
+  if (op == 0) {
+    c = Camera(float3(a[0], a[1], a[2]), float3(b[0], b[1], b[2]), float3(c3[0], c3[1], c3[2]));
+  } else {
+    c = cam_from(st);
+    if (op == 1) c.rotate(x, y);
+    else if (op == 2) c.resetPosition(float3(a[0], a[1], a[2]));
+    else if (op == 3) c.resetTarget(float3(a[0], a[1], a[2]));
+    else if (op == 4) c.setLockUp(x != 0.0f);
+    else if (op == 5) c.zoom(x);
+  }
+  cam_to(c, st);
+  if (view_inv) {
+    float4x4 vi = inverse4x4(c.lookAtMatrix());
+    std::memcpy(view_inv, vi.m, 64);
+  }
+}
 }  // extern "C"

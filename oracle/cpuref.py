@@ -59,6 +59,7 @@ def lib():
         L.cpuref_primary_rays.argtypes = [vp, C.c_int, C.c_int, vp]
         L.cpuref_fnv1a64.restype = C.c_uint64
         L.cpuref_sdf_points.argtypes = [vp, i64, vp, i64, vp, i64, vp, C.c_int]
+        L.cpuref_cam_op.argtypes = [vp, C.c_int, vp, vp, vp, f32, f32, vp]
         L.cpuref_fnv1a64.argtypes = [vp, i64]
         _lib = L
     return _lib
@@ -331,3 +332,34 @@ def subdivide(vpos4, idx, levels: int):
             J += [a, ab, ca, ab, b, bc, ca, bc, c, ab, bc, ca]
         I = J
     return np.array(V, np.float32).reshape(-1, 4), np.array(I, np.uint32)
+
+
+# ------------------------------------------------------------ orbit camera --
+class RefCamera:
+    """The reference Camera (camera.cpp:1-72) over an rt_camera_state-shaped
+    array of 15 words; every op returns inverse4x4(lookAtMatrix())."""
+
+    def __init__(self, pos, target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)):
+        self.st = np.zeros(15, np.float32)
+        self.view_inv = self._op(0, pos, target, up)
+
+    def _op(self, op, a=None, b=None, c=None, x=0.0, y=0.0):
+        arr = [None if v is None else np.ascontiguousarray(v, np.float32) for v in (a, b, c)]
+        vi = np.zeros(16, np.float32)
+        lib().cpuref_cam_op(_p(self.st), op, *[_p(v) for v in arr], float(x), float(y), _p(vi))
+        return vi
+
+    def rotate(self, dx, dy):
+        self.view_inv = self._op(1, x=dx, y=dy)
+
+    def resetPosition(self, p):
+        self.view_inv = self._op(2, a=p)
+
+    def resetTarget(self, t):
+        self.view_inv = self._op(3, a=t)
+
+    def setLockUp(self, on):
+        self.view_inv = self._op(4, x=1.0 if on else 0.0)
+
+    def zoom(self, wheel):
+        self.view_inv = self._op(5, x=wheel)

@@ -9,7 +9,7 @@
 //
 //   rt_render <input> [--size W H] [--pos x y z] [--mode normal|lambert|color]
 //             [--plane 0|1] [--shadows 0|1] [--reflections 0|1] [--frames N]
-//             [--ppm out.ppm]
+//             [--ppm out.ppm] [--png out.png] [--drag dx dy] [--zoom notches]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -42,7 +42,8 @@ int usage() {
   std::fprintf(stderr,
                "usage: rt_render <input.obj|.grid|.octree> [--size W H] [--pos x y z]\n"
                "       [--mode normal|lambert|color] [--plane 0|1] [--shadows 0|1]\n"
-               "       [--reflections 0|1] [--frames N] [--ppm out.ppm]\n");
+               "       [--reflections 0|1] [--frames N] [--ppm out.ppm] [--png out.png]\n"
+               "       [--drag dx dy] [--zoom notches]\n");
   return 2;
 }
 
@@ -57,7 +58,8 @@ int main(int argc, char **argv) {
   renderer.shadingMode = rtamd::ShadingMode::Lambert;
   bool plane = true;
   int frames = 1;
-  const char *ppm = nullptr;
+  const char *ppm = nullptr, *png = nullptr;
+  float drag_dx = 0.0f, drag_dy = 0.0f, zoom = 0.0f;
   for (int i = 2; i < argc; ++i) {
     const std::string a = argv[i];
     auto need = [&](int k) {
@@ -93,6 +95,16 @@ int main(int argc, char **argv) {
     } else if (a == "--ppm") {
       need(1);
       ppm = argv[++i];
+    } else if (a == "--png") {
+      need(1);
+      png = argv[++i];
+    } else if (a == "--drag") {  // a mouse drag in the viewer: Camera::rotate(-dx, -dy)
+      need(2);
+      drag_dx = std::strtof(argv[++i], nullptr);
+      drag_dy = std::strtof(argv[++i], nullptr);
+    } else if (a == "--zoom") {  // mouse-wheel notches
+      need(1);
+      zoom = std::strtof(argv[++i], nullptr);
     } else {
       return usage();
     }
@@ -124,7 +136,9 @@ int main(int argc, char **argv) {
 
     rtamd::FrameBuffer fb;
     fb.resize(W, H);
-    const rtamd::Camera camera(pos, {0.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f});
+    rtamd::Camera camera(pos, {0.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f});
+    if (drag_dx != 0.0f || drag_dy != 0.0f) camera.rotate(-drag_dx, -drag_dy);
+    if (zoom != 0.0f) camera.zoom(zoom);
     const rtamd::float4x4 projInv = rtamd::projInverse(45.0f, (float)W / (float)H, 0.01f, 100.0f);
     const rtamd::SceneUnion full(*scene, rtamd::Plane{{0.0f, 1.0f, 0.0f}, planeY});
     double total_ms = 0.0;
@@ -140,6 +154,7 @@ int main(int argc, char **argv) {
       covered += std::isfinite(fb.t[i]) ? 1 : 0;
     }
     if (ppm) write_ppm(ppm, fb);
+    if (png) fb.savePNG(png);
     std::printf(
         "{\"input\": \"%s\", \"width\": %u, \"height\": %u, \"frames\": %d, \"hash\": \"%016llx\", "
         "\"covered\": %lld, \"kernel_ms\": %.4f}\n",

@@ -1114,6 +1114,56 @@ int rtx_wave_stamps(rt_scene *s, const rt_render_params *params, int32_t W, int3
   return RT_OK;
 }
 
+// ---- orbit camera + image output (host-only; rt_host.cpp) ----------------
+static_assert(sizeof(rt_camera_state) == sizeof(rth::CamState), "camera state layout");
+#define CAM(c) (*reinterpret_cast<rth::CamState *>(c))
+int rt_camera_init(const float pos[3], const float target[3], const float up[3], rt_camera_state *c) {
+  if (!pos || !target || !up || !c) return set_err(RT_E_INVALID, "bad arguments");
+  rth::cam_init(CAM(c), pos, target, up);
+  return RT_OK;
+}
+int rt_camera_rotate(rt_camera_state *c, float dx, float dy) {
+  if (!c) return set_err(RT_E_INVALID, "camera is NULL");
+  rth::cam_rotate(CAM(c), dx, dy);
+  return RT_OK;
+}
+int rt_camera_reset_position(rt_camera_state *c, const float pos[3]) {
+  if (!c || !pos) return set_err(RT_E_INVALID, "bad arguments");
+  rth::cam_reset_position(CAM(c), pos);
+  return RT_OK;
+}
+int rt_camera_reset_target(rt_camera_state *c, const float target[3]) {
+  if (!c || !target) return set_err(RT_E_INVALID, "bad arguments");
+  rth::cam_reset_target(CAM(c), target);
+  return RT_OK;
+}
+int rt_camera_set_lock_up(rt_camera_state *c, int on) {
+  if (!c) return set_err(RT_E_INVALID, "camera is NULL");
+  rth::cam_set_lock_up(CAM(c), on != 0);
+  return RT_OK;
+}
+int rt_camera_zoom(rt_camera_state *c, float wheel) {
+  if (!c) return set_err(RT_E_INVALID, "camera is NULL");
+  rth::cam_zoom(CAM(c), wheel);
+  return RT_OK;
+}
+int rt_camera_basis(const rt_camera_state *c, float up[3], float right[3], float forward[3]) {
+  if (!c) return set_err(RT_E_INVALID, "camera is NULL");
+  rth::cam_basis(*reinterpret_cast<const rth::CamState *>(c), up, right, forward);
+  return RT_OK;
+}
+int rt_camera_view_inverse(const rt_camera_state *c, float view_inv[16]) {
+  if (!c || !view_inv) return set_err(RT_E_INVALID, "bad arguments");
+  rth::cam_view_inverse(*reinterpret_cast<const rth::CamState *>(c), view_inv);
+  return RT_OK;
+}
+#undef CAM
+int rt_write_png(const char *path, const uint32_t *color, int32_t W, int32_t H) {
+  std::string err;
+  if (!rth::write_png(path, color, W, H, err)) return set_err(RT_E_IO, err);
+  return RT_OK;
+}
+
 // Diagnostic: primary ray directions as the render kernel computes them (host buffer [H][W][3]).
 int rtx_eye_rays(const rt_render_params *p, int32_t W, int32_t H, float *out) {
   int rc = check_params(p, W, H);

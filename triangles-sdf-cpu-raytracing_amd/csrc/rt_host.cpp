@@ -604,9 +604,11 @@ static inline Q qmul(Q a, Q b) {  // quaternion.hpp:40-45
 }
 }  // namespace
 
-void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
-                     float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]) {
-  V3 P{pos[0], pos[1], pos[2]}, T{target[0], target[1], target[2]}, U{up[0], up[1], up[2]};
+namespace {
+// Camera::updateOrientation (camera.cpp:36-62): the orientation quaternion of
+// lookAt(pos, target, up), left un-normalised (camera.cpp:61 discards the
+// normalize result).
+Q orientation_of(V3 P, V3 T, V3 U) {
   M4 m = look_at(P, T, U);
   Q q;
   if (m.at(2, 2) < 0) {
@@ -626,12 +628,175 @@ void camera_matrices(const float pos[3], const float target[3], const float up[3
       q = {m.at(1, 2) - m.at(2, 1), m.at(2, 0) - m.at(0, 2), m.at(0, 1) - m.at(1, 0), t};
     }
   }
-  // up() = normalize(rotateVector({0,1,0}, q)) (quaternion.hpp:47-52)
-  Q p{0.0f, 1.0f, 0.0f, 0.0f}, c{-q.x, -q.y, -q.z, q.w};
-  Q r = qmul(qmul(q, p), c);
-  V3 up2 = nrm(V3{r.x, r.y, r.z});
-  M4 view = look_at(P, T, up2);
+  return q;
+}
+// rotateVector (quaternion.hpp:47-52): q * (v, 0) * conjugate(q)
+V3 rotate_vector(V3 v, Q q) {
+  const Q p{v.x, v.y, v.z, 0.0f}, c{-q.x, -q.y, -q.z, q.w};
+  const Q r = qmul(qmul(q, p), c);
+  return {r.x, r.y, r.z};
+}
+// angleAxis (quaternion.hpp:54-70)
+Q angle_axis(float angle, V3 axis) {
+  const V3 n = nrm(axis);
+  const float half = angle * 0.5f;
+  Q q;
+  q.w = std::cos(half);
+  q.x = n.x * std::sin(half);
+  q.y = n.y * std::sin(half);
+  q.z = n.z * std::sin(half);
+  return q;
+}
+V3 v3(const float *p) { return {p[0], p[1], p[2]}; }
+void put(float *o, V3 v) { o[0] = v.x; o[1] = v.y; o[2] = v.z; }
+Q q_of(const CamState &c) { return {c.q[0], c.q[1], c.q[2], c.q[3]}; }
+void set_q(CamState &c, Q q) { c.q[0] = q.x; c.q[1] = q.y; c.q[2] = q.z; c.q[3] = q.w; }
+V3 cam_up_v(const CamState &c) { return nrm(rotate_vector({0.0f, 1.0f, 0.0f}, q_of(c))); }     // camera.hpp:29-31
+V3 cam_right_v(const CamState &c) { return nrm(rotate_vector({1.0f, 0.0f, 0.0f}, q_of(c))); }  // camera.hpp:32-34
+V3 cam_forward_v(const CamState &c) { return nrm(sub(v3(c.target), v3(c.pos))); }              // camera.hpp:35-37
+float len3(V3 a) { return std::sqrt(dot3(a, a)); }
+}  // namespace
+
+void cam_init(CamState &c, const float pos[3], const float target[3], const float up[3]) {
+  c = CamState{};
+  put(c.pos, v3(pos));
+  put(c.target, v3(target));
+  set_q(c, orientation_of(v3(pos), v3(target), v3(up)));
+  c.sens = 0.01f;  // camera.hpp:55
+}
+
+// Camera::rotate + updateVectors (camera.cpp:5-34)
+void cam_rotate(CamState &c, float dx, float dy) {
+  const float pitch = dy * c.sens, yaw = dx * c.sens;
+  const Q q_yaw = angle_axis(yaw, cam_up_v(c));
+  const Q q_pitch = angle_axis(pitch, cam_right_v(c));
+  const Q r = qmul(qmul(q_pitch, q_yaw), q_of(c));
+  // Quaternion::normalized (quaternion.hpp:30-33): / length of the float4
+  const float n = std::sqrt(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+  set_q(c, Q{r.x / n, r.y / n, r.z / n, r.w / n});
+  // updateVectors: keep the distance to the target, move along the new forward
+  const V3 f = nrm(rotate_vector({0.0f, 0.0f, -1.0f}, q_of(c)));
+  const V3 T = v3(c.target);
+  const float dist = len3(sub(T, v3(c.pos)));
+  put(c.pos, sub(T, V3{f.x * dist, f.y * dist, f.z * dist}));
+  if (c.lock) set_q(c, orientation_of(v3(c.pos), T, v3(c.locked)));
+}
+
+void cam_reset_position(CamState &c, const float pos[3]) {  // camera.cpp:64-67
+  const V3 up = cam_up_v(c);
+  put(c.pos, v3(pos));
+  set_q(c, orientation_of(v3(c.pos), v3(c.target), up));
+}
+
+void cam_reset_target(CamState &c, const float target[3]) {  // camera.cpp:69-72
+  const V3 up = cam_up_v(c);
+  put(c.target, v3(target));
+  set_q(c, orientation_of(v3(c.pos), v3(c.target), up));
+}
+
+void cam_set_lock_up(CamState &c, bool on) {  // camera.hpp:39-44
+  if (!c.lock && on) put(c.locked, cam_up_v(c));
+  c.lock = on ? 1 : 0;
+}
+
+// The viewer's mouse wheel (main.cpp:283-288): move along forward by
+// wheel * distance / 25.
+void cam_zoom(CamState &c, float wheel) {
+  const float dist = len3(sub(v3(c.target), v3(c.pos)));
+  const float r = wheel * dist / 25.0f;
+  const V3 f = cam_forward_v(c);
+  const V3 P = v3(c.pos);
+  const float np[3] = {P.x + f.x * r, P.y + f.y * r, P.z + f.z * r};
+  cam_reset_position(c, np);
+}
+
+void cam_basis(const CamState &c, float up[3], float right[3], float forward[3]) {
+  if (up) put(up, cam_up_v(c));
+  if (right) put(right, cam_right_v(c));
+  if (forward) put(forward, cam_forward_v(c));
+}
+
+// inverse4x4(lookAtMatrix()) (camera.hpp:24-26, raytracing.cpp:74-75)
+void cam_view_inverse(const CamState &c, float view_inv[16]) {
+  M4 view = look_at(v3(c.pos), v3(c.target), cam_up_v(c));
   invert(view, view_inv);
+}
+
+// ------------------------------------------------------------------ PNG ---
+namespace {
+uint32_t crc32(const uint8_t *p, size_t n, uint32_t c = 0xFFFFFFFFu) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t v = i;
+      for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xEDB88320u ^ (v >> 1) : v >> 1;
+      table[i] = v;
+    }
+    init = true;
+  }
+  for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c;
+}
+void be32(std::vector<uint8_t> &o, uint32_t v) {
+  o.push_back((uint8_t)(v >> 24)); o.push_back((uint8_t)(v >> 16));
+  o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v);
+}
+void chunk(std::vector<uint8_t> &o, const char *type, const std::vector<uint8_t> &data) {
+  be32(o, (uint32_t)data.size());
+  const size_t start = o.size();
+  o.insert(o.end(), type, type + 4);
+  o.insert(o.end(), data.begin(), data.end());
+  be32(o, crc32(o.data() + start, o.size() - start) ^ 0xFFFFFFFFu);
+}
+}  // namespace
+
+bool write_png(const char *path, const uint32_t *rgba, int32_t W, int32_t H, std::string &err) {
+  if (!path || !rgba || W <= 0 || H <= 0) { err = "bad arguments"; return false; }
+  std::vector<uint8_t> raw;  // filter byte 0 + RGBA per row
+  raw.reserve((size_t)H * (1 + 4 * (size_t)W));
+  for (int32_t y = 0; y < H; ++y) {
+    raw.push_back(0);
+    for (int32_t x = 0; x < W; ++x) {
+      const uint32_t c = rgba[(size_t)y * W + x];
+      raw.push_back((uint8_t)c); raw.push_back((uint8_t)(c >> 8));
+      raw.push_back((uint8_t)(c >> 16)); raw.push_back((uint8_t)(c >> 24));
+    }
+  }
+  std::vector<uint8_t> z{0x78, 0x01};  // zlib header, stored blocks
+  uint32_t a = 1, b = 0;
+  for (size_t off = 0; off < raw.size() || off == 0; off += 65535) {
+    const size_t n = std::min<size_t>(65535, raw.size() - off);
+    z.push_back(off + n >= raw.size() ? 1 : 0);
+    z.push_back((uint8_t)n); z.push_back((uint8_t)(n >> 8));
+    z.push_back((uint8_t)~n); z.push_back((uint8_t)(~n >> 8));
+    z.insert(z.end(), raw.begin() + off, raw.begin() + off + n);
+    if (raw.empty()) break;
+  }
+  for (uint8_t v : raw) { a = (a + v) % 65521u; b = (b + a) % 65521u; }
+  be32(z, (b << 16) | a);
+  std::vector<uint8_t> png{0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+  std::vector<uint8_t> ihdr;
+  be32(ihdr, (uint32_t)W);
+  be32(ihdr, (uint32_t)H);
+  const uint8_t rest[5] = {8, 6, 0, 0, 0};  // 8-bit RGBA, deflate, no filter method ext, no interlace
+  ihdr.insert(ihdr.end(), rest, rest + 5);
+  chunk(png, "IHDR", ihdr);
+  chunk(png, "IDAT", z);
+  chunk(png, "IEND", {});
+  FILE *f = std::fopen(path, "wb");
+  if (!f) { err = std::string("cannot write ") + path; return false; }
+  const size_t wrote = std::fwrite(png.data(), 1, png.size(), f);
+  std::fclose(f);
+  if (wrote != png.size()) { err = "short write"; return false; }
+  return true;
+}
+
+void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
+                     float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]) {
+  CamState c;
+  cam_init(c, pos, target, up);
+  cam_view_inverse(c, view_inv);
   // perspectiveMatrix(fovy, aspect, near, far)
   M4 pr{};
   const float ymax = znear * std::tan(fovy * 3.14159265358979323846f / 360.0f);

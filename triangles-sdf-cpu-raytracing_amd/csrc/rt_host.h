@@ -69,6 +69,26 @@ using SdfQuery = bool (*)(void *ctx, const float *p3, int64_t n, float *out, std
 bool build_sdf_octree(SdfQuery query, void *ctx, int depth, std::vector<uint8_t> &nodes36,
                       std::string &err);
 
+// Camera (camera.hpp:7-61, camera.cpp:1-72): the viewer's orbit camera.
+// Same memory layout as rt_camera_state (include/rtamd.h).
+struct CamState {
+  float pos[3], target[3], q[4];
+  float sens;
+  int32_t lock;
+  float locked[3];
+};
+void cam_init(CamState &c, const float pos[3], const float target[3], const float up[3]);
+void cam_rotate(CamState &c, float dx, float dy);
+void cam_reset_position(CamState &c, const float pos[3]);
+void cam_reset_target(CamState &c, const float target[3]);
+void cam_set_lock_up(CamState &c, bool on);
+void cam_zoom(CamState &c, float wheel);
+void cam_basis(const CamState &c, float up[3], float right[3], float forward[3]);
+void cam_view_inverse(const CamState &c, float view_inv[16]);
+
+// 8-bit RGBA PNG (stored deflate blocks: no compression library needed).
+bool write_png(const char *path, const uint32_t *rgba, int32_t W, int32_t H, std::string &err);
+
 void camera_matrices(const float pos[3], const float target[3], const float up[3], float fovy,
                      float aspect, float znear, float zfar, float view_inv[16], float proj_inv[16]);
 

@@ -44,6 +44,12 @@ class Tile(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+class CameraState(C.Structure):
+    """rt_camera_state (include/rtamd.h)."""
+    _fields_ = [("position", C.c_float * 3), ("target", C.c_float * 3), ("orientation", C.c_float * 4),
+                ("sensitivity", C.c_float), ("lock_up", C.c_int32), ("locked_up", C.c_float * 3)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "rt_last_error": (C.c_char_p, []),
@@ -89,6 +95,15 @@ _SIGS = {
     "rt_sdf_mesh_destroy": (C.c_int, [C.c_void_p]),
     "rt_mesh_subdivide": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p,
                                     C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)]),
+    "rt_camera_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(CameraState)]),
+    "rt_camera_rotate": (C.c_int, [C.POINTER(CameraState), C.c_float, C.c_float]),
+    "rt_camera_reset_position": (C.c_int, [C.POINTER(CameraState), C.c_void_p]),
+    "rt_camera_reset_target": (C.c_int, [C.POINTER(CameraState), C.c_void_p]),
+    "rt_camera_set_lock_up": (C.c_int, [C.POINTER(CameraState), C.c_int]),
+    "rt_camera_zoom": (C.c_int, [C.POINTER(CameraState), C.c_float]),
+    "rt_camera_basis": (C.c_int, [C.POINTER(CameraState), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_camera_view_inverse": (C.c_int, [C.POINTER(CameraState), C.c_void_p]),
+    "rt_write_png": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32]),
 }
 
 EXPORTED = tuple(_SIGS)

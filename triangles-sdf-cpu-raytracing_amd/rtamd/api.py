@@ -23,7 +23,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (RT_FLAG_CLEAR, RenderParams, RtError, Tile, check, lib)
+from ._lib import (RT_FLAG_CLEAR, CameraState, RenderParams, RtError, Tile, check, lib)
 
 __all__ = [
     "ShadingMode", "SimpleMesh", "FrameBuffer", "Camera", "Renderer", "HitInfo", "IScene",
@@ -118,22 +118,68 @@ def render_params(cam_pos, view_inv, proj_inv, light=(2.0, 2.0, 2.0), mode=Shadi
 
 
 class Camera:
-    """Camera(position, target, up) (src/camera.hpp:7-61): view matrix only."""
+    """Camera (src/camera.hpp:7-61, src/camera.cpp:1-72): the viewer's orbit
+    camera -- position, target and an orientation quaternion -- through the
+    host-side C ABI (rt_camera_*), bit-identical to the reference's float math."""
 
-    def __init__(self, position, target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)):
-        self._pos = np.asarray(position, np.float32)
-        self._target = np.asarray(target, np.float32)
-        self._up = np.asarray(up, np.float32)
+    def __init__(self, position=(0.0, 0.0, 2.5), target=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)):
+        self._s = CameraState()
+        p, t, u = (np.ascontiguousarray(x, np.float32) for x in (position, target, up))
+        check(lib().rt_camera_init(_p(p), _p(t), _p(u), C.byref(self._s)))
 
     def position(self):
-        return self._pos.copy()
+        return np.array(self._s.position, np.float32)
 
     def target(self):
-        return self._target.copy()
+        return np.array(self._s.target, np.float32)
+
+    def _basis(self):
+        u, r, f = (np.zeros(3, np.float32) for _ in range(3))
+        check(lib().rt_camera_basis(C.byref(self._s), _p(u), _p(r), _p(f)))
+        return u, r, f
+
+    def up(self):
+        return self._basis()[0]
+
+    def right(self):
+        return self._basis()[1]
+
+    def forward(self):
+        return self._basis()[2]
+
+    def sensetivity(self) -> float:  # (sic) camera.hpp:38
+        return float(self._s.sensitivity)
+
+    def rotate(self, dx: float, dy: float):
+        """Camera::rotate (camera.cpp:5-20); the viewer calls rotate(-dx, -dy) on a drag."""
+        check(lib().rt_camera_rotate(C.byref(self._s), float(dx), float(dy)))
+
+    def resetPosition(self, position):
+        p = np.ascontiguousarray(position, np.float32)
+        check(lib().rt_camera_reset_position(C.byref(self._s), _p(p)))
+
+    def resetTarget(self, target):
+        t = np.ascontiguousarray(target, np.float32)
+        check(lib().rt_camera_reset_target(C.byref(self._s), _p(t)))
+
+    def setLockUp(self, on: bool):
+        check(lib().rt_camera_set_lock_up(C.byref(self._s), int(bool(on))))
+
+    def isLockedUp(self) -> bool:
+        return bool(self._s.lock_up)
+
+    def zoom(self, wheel: float):
+        """The viewer's mouse wheel (main.cpp:281-288)."""
+        check(lib().rt_camera_zoom(C.byref(self._s), float(wheel)))
 
     def view_inv(self):
-        vi, _ = camera_matrices(self._pos, self._target, self._up)
+        """inverse4x4(lookAtMatrix()), column-major float32[16]."""
+        vi = np.zeros(16, np.float32)
+        check(lib().rt_camera_view_inverse(C.byref(self._s), _p(vi)))
         return vi
+
+    def state(self) -> CameraState:
+        return self._s
 
 
 class FrameBuffer:
@@ -157,6 +203,11 @@ class FrameBuffer:
     @property
     def height(self):
         return self.color.shape[0]
+
+    def save_png(self, path: str):
+        """The colour buffer as an 8-bit RGBA PNG (rt_write_png)."""
+        c = np.ascontiguousarray(self.color, np.uint32)
+        check(lib().rt_write_png(str(path).encode(), _p(c), self.width, self.height))
 
 
 @dataclass
