@@ -232,6 +232,11 @@ int rt_camera_view_inverse(const rt_camera_state *c, float view_inv[16]);
 /* Write a colour buffer (W*H packed RGBA8, R in the low byte, row 0 = top) as
  * an 8-bit RGBA PNG (what the viewer shows, main.cpp:239-242). */
 int rt_write_png(const char *path, const uint32_t *color, int32_t W, int32_t H);
+/* cmesh4::SaveMeshToObj (src/core/mesh.cpp:14-63), byte for byte: v / vt / vn
+ * per vertex with std::to_string, faces "f i/i/i". vnorm4 (4 per vertex) and
+ * vtex2 (2 per vertex) may be NULL: fix_missing's defaults (0,0,1) / (0,0). */
+int rt_save_obj(const char *path, const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                const float *vnorm4, const float *vtex2);
 
 #ifdef __cplusplus
 }

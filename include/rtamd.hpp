@@ -5,6 +5,7 @@
 //   reference (src/...)                            here (namespace rtamd)
 //   --------------------------------------------   ------------------------------------
 //   cmesh4::LoadMeshFromObj + loadAndScale          LoadMeshFromObj(path, /*scale=*/true)
+//   cmesh4::SaveMeshToObj(path, mesh)               SaveMeshToObj(path, mesh)
 //   BVHBuilder b; b.perform(std::move(mesh));       BVHBuilder b; b.perform(mesh);
 //   SDFGrid g; loadSDFGrid(g, path);                SDFGrid g; loadSDFGrid(g, path);
 //   SDFOctree o; loadSDFOctree(o, path);            SDFOctree o; loadSDFOctree(o, path);
@@ -72,6 +73,12 @@ inline SimpleMesh LoadMeshFromObj(const std::string &path, bool scale = true) {
   m.indices.resize((size_t)ni);
   check(rt_load_obj(path.c_str(), scale ? 1 : 0, m.vPos4f.data(), &nv, m.indices.data(), &ni));
   return m;
+}
+
+// cmesh4::SaveMeshToObj (core/mesh.cpp:14-63); normals / texcoords default as fix_missing.
+inline void SaveMeshToObj(const std::string &path, const SimpleMesh &m) {
+  check(rt_save_obj(path.c_str(), m.vPos4f.data(), (int64_t)(m.vPos4f.size() / 4), m.indices.data(),
+                    (int64_t)m.indices.size(), nullptr, nullptr));
 }
 
 // FrameBuffer {Image2D<uint32_t> color; Image2D<float> t;} (raytracing.hpp:9-20)

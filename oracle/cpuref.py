@@ -363,3 +363,22 @@ class RefCamera:
 
     def zoom(self, wheel):
         self.view_inv = self._op(5, x=wheel)
+
+
+def save_obj_text(vpos4, idx, vnorm4=None, vtex2=None) -> bytes:
+    """cmesh4::SaveMeshToObj (src/core/mesh.cpp:14-63) restated: std::to_string
+    is printf "%f" of the float promoted to double; section order v, vt, vn,
+    "s off", faces "f i/i/i" (1-based). Missing normals / texture coordinates
+    take fix_missing's defaults (mesh.cpp:143-160)."""
+    v = np.asarray(vpos4, np.float32).reshape(-1, 4)
+    n = np.tile(np.float32([0, 0, 1, 0]), (len(v), 1)) if vnorm4 is None else np.asarray(vnorm4, np.float32)
+    t = np.zeros((len(v), 2), np.float32) if vtex2 is None else np.asarray(vtex2, np.float32)
+    f = lambda x: "%f" % float(x)
+    out = ["# obj file created by custom obj loader\n", "o MainModel\n"]
+    out += ["v %s %s %s\n" % (f(p[0]), f(p[1]), f(p[2])) for p in v]
+    out += ["vt %s %s\n" % (f(p[0]), f(p[1])) for p in t.reshape(-1, 2)]
+    out += ["vn %s %s %s\n" % (f(p[0]), f(p[1]), f(p[2])) for p in n.reshape(-1, 4)]
+    out.append("s off\n")
+    ii = np.asarray(idx, np.uint32).reshape(-1, 3).astype(np.int64) + 1
+    out += ["f %d/%d/%d %d/%d/%d %d/%d/%d\n" % (a, a, a, b, b, b, c, c, c) for a, b, c in ii]
+    return "".join(out).encode()

@@ -71,3 +71,14 @@ def test_cli_reproduces_golden_hash(gpu, name, W, H, mode):
     key = (name, W, H, mode)
     if key in S.COVERAGE:
         assert out["covered"] == S.COVERAGE[key]
+
+
+def test_cli_save_obj_matches_reference_writer(rt, ref, tmp_path):
+    """rtamd::SaveMeshToObj through the C++ wrapper: the loaded, scaled mesh
+    written byte for byte as cmesh4::SaveMeshToObj would (mesh.cpp:14-63).
+    The file is written before the scene upload, so this runs without a GPU."""
+    out = tmp_path / "cube_out.obj"
+    subprocess.run([CLI, data.path("cube.obj"), "--size", "8", "8", "--save-obj", str(out)],
+                   capture_output=True, text=True, timeout=120)
+    v, i = ref.load_obj(data.path("cube.obj"))
+    assert out.read_bytes() == ref.save_obj_text(v, i)

@@ -10,6 +10,7 @@
 //   rt_render <input> [--size W H] [--pos x y z] [--mode normal|lambert|color]
 //             [--plane 0|1] [--shadows 0|1] [--reflections 0|1] [--frames N]
 //             [--ppm out.ppm] [--png out.png] [--drag dx dy] [--zoom notches]
+//             [--save-obj out.obj]   (the loaded, scaled mesh via SaveMeshToObj)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -43,7 +44,7 @@ int usage() {
                "usage: rt_render <input.obj|.grid|.octree> [--size W H] [--pos x y z]\n"
                "       [--mode normal|lambert|color] [--plane 0|1] [--shadows 0|1]\n"
                "       [--reflections 0|1] [--frames N] [--ppm out.ppm] [--png out.png]\n"
-               "       [--drag dx dy] [--zoom notches]\n");
+               "       [--drag dx dy] [--zoom notches] [--save-obj out.obj]\n");
   return 2;
 }
 
@@ -58,7 +59,7 @@ int main(int argc, char **argv) {
   renderer.shadingMode = rtamd::ShadingMode::Lambert;
   bool plane = true;
   int frames = 1;
-  const char *ppm = nullptr, *png = nullptr;
+  const char *ppm = nullptr, *png = nullptr, *save_obj = nullptr;
   float drag_dx = 0.0f, drag_dy = 0.0f, zoom = 0.0f;
   for (int i = 2; i < argc; ++i) {
     const std::string a = argv[i];
@@ -98,6 +99,9 @@ int main(int argc, char **argv) {
     } else if (a == "--png") {
       need(1);
       png = argv[++i];
+    } else if (a == "--save-obj") {
+      need(1);
+      save_obj = argv[++i];
     } else if (a == "--drag") {  // a mouse drag in the viewer: Camera::rotate(-dx, -dy)
       need(2);
       drag_dx = std::strtof(argv[++i], nullptr);
@@ -119,6 +123,7 @@ int main(int argc, char **argv) {
       float ymin = INFINITY;
       for (size_t v = 0; v < mesh.vPos4f.size(); v += 4) ymin = std::min(ymin, mesh.vPos4f[v + 1]);
       planeY = ymin;
+      if (save_obj) rtamd::SaveMeshToObj(save_obj, mesh);
       auto b = std::make_unique<rtamd::BVHBuilder>();
       b->perform(mesh);
       scene = std::move(b);

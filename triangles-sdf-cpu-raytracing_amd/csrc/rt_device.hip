@@ -1164,6 +1164,15 @@ int rt_write_png(const char *path, const uint32_t *color, int32_t W, int32_t H) 
   return RT_OK;
 }
 
+int rt_save_obj(const char *path, const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+                const float *vnorm4, const float *vtex2) {
+  std::string err;
+  if (nverts < 0 || nidx < 0) return set_err(RT_E_INVALID, "bad counts");
+  if (!rth::save_obj(path, vpos4, nverts, idx, nidx, vnorm4, vtex2, err))
+    return set_err(err.rfind("cannot", 0) == 0 || err == "short write" ? RT_E_IO : RT_E_INVALID, err);
+  return RT_OK;
+}
+
 // Diagnostic: primary ray directions as the render kernel computes them (host buffer [H][W][3]).
 int rtx_eye_rays(const rt_render_params *p, int32_t W, int32_t H, float *out) {
   int rc = check_params(p, W, H);

@@ -722,6 +722,41 @@ void cam_view_inverse(const CamState &c, float view_inv[16]) {
   invert(view, view_inv);
 }
 
+// ------------------------------------------------------------ OBJ writer ---
+// cmesh4::SaveMeshToObj (core/mesh.cpp:14-63): "v/vt/vn" records per vertex
+// with std::to_string (printf "%f"), faces "f i/i/i" (1-based), in the
+// reference's section order. Missing normals / texture coordinates take
+// fix_missing's defaults (mesh.cpp:143-160): (0,0,1) and (0,0).
+bool save_obj(const char *path, const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+              const float *vnorm4, const float *vtex2, std::string &err) {
+  if (!path || (!vpos4 && nverts) || (!idx && nidx) || nidx % 3 != 0) { err = "bad arguments"; return false; }
+  FILE *f = std::fopen(path, "wb");
+  if (!f) { err = std::string("cannot create ") + path; return false; }
+  auto num = [](float x) { return std::to_string(x); };
+  std::string v, tc, n, fc;
+  for (int64_t i = 0; i < nverts; ++i) {
+    const float *p = vpos4 + 4 * i;
+    v += "v " + num(p[0]) + " " + num(p[1]) + " " + num(p[2]) + "\n";
+    const float nx = vnorm4 ? vnorm4[4 * i] : 0.0f, ny = vnorm4 ? vnorm4[4 * i + 1] : 0.0f,
+                nz = vnorm4 ? vnorm4[4 * i + 2] : 1.0f;
+    n += "vn " + num(nx) + " " + num(ny) + " " + num(nz) + "\n";
+    tc += "vt " + num(vtex2 ? vtex2[2 * i] : 0.0f) + " " + num(vtex2 ? vtex2[2 * i + 1] : 0.0f) + "\n";
+  }
+  for (int64_t t = 0; t < nidx / 3; ++t) {
+    fc += "f";
+    for (int k = 0; k < 3; ++k) {
+      const std::string q = std::to_string(idx[3 * t + k] + 1);
+      fc += " " + q + "/" + q + "/" + q;
+    }
+    fc += "\n";
+  }
+  const std::string all = "# obj file created by custom obj loader\no MainModel\n" + v + tc + n + "s off\n" + fc;
+  const size_t wrote = std::fwrite(all.data(), 1, all.size(), f);
+  std::fclose(f);
+  if (wrote != all.size()) { err = "short write"; return false; }
+  return true;
+}
+
 // ------------------------------------------------------------------ PNG ---
 namespace {
 uint32_t crc32(const uint8_t *p, size_t n, uint32_t c = 0xFFFFFFFFu) {

@@ -86,6 +86,10 @@ void cam_zoom(CamState &c, float wheel);
 void cam_basis(const CamState &c, float up[3], float right[3], float forward[3]);
 void cam_view_inverse(const CamState &c, float view_inv[16]);
 
+// cmesh4::SaveMeshToObj (core/mesh.cpp:14-63); vnorm4 / vtex2 may be NULL.
+bool save_obj(const char *path, const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
+              const float *vnorm4, const float *vtex2, std::string &err);
+
 // 8-bit RGBA PNG (stored deflate blocks: no compression library needed).
 bool write_png(const char *path, const uint32_t *rgba, int32_t W, int32_t H, std::string &err);
 

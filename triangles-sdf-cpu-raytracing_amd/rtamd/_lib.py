@@ -104,6 +104,8 @@ _SIGS = {
     "rt_camera_basis": (C.c_int, [C.POINTER(CameraState), C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_camera_view_inverse": (C.c_int, [C.POINTER(CameraState), C.c_void_p]),
     "rt_write_png": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32]),
+    "rt_save_obj": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
+                              C.c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -29,7 +29,7 @@ __all__ = [
     "ShadingMode", "SimpleMesh", "FrameBuffer", "Camera", "Renderer", "HitInfo", "IScene",
     "BVHBuilder", "SDFGrid", "SDFOctree", "Plane", "SceneUnion", "load_mesh_from_obj",
     "load_sdf_grid", "load_sdf_octree", "camera_matrices", "render_params", "RtError",
-    "RT_FLAG_CLEAR", "Tile", "device_count", "SDFMesh", "subdivide_mesh",
+    "RT_FLAG_CLEAR", "Tile", "device_count", "SDFMesh", "subdivide_mesh", "save_mesh_to_obj",
 ]
 
 
@@ -66,6 +66,15 @@ def load_mesh_from_obj(path: str, scale: bool = True) -> SimpleMesh:
     i = np.empty(ni.value, np.uint32)
     check(L.rt_load_obj(path.encode(), int(scale), _p(v), C.byref(nv), _p(i), C.byref(ni)))
     return SimpleMesh(v, i)
+
+
+def save_mesh_to_obj(path: str, mesh: SimpleMesh, normals=None, texcoords=None):
+    """cmesh4::SaveMeshToObj (src/core/mesh.cpp:14-63), byte for byte."""
+    v = np.ascontiguousarray(mesh.vPos4f, np.float32)
+    i = np.ascontiguousarray(mesh.indices, np.uint32)
+    n = None if normals is None else np.ascontiguousarray(normals, np.float32)
+    t = None if texcoords is None else np.ascontiguousarray(texcoords, np.float32)
+    check(lib().rt_save_obj(str(path).encode(), _p(v), len(v), _p(i), len(i), _p(n), _p(t)))
 
 
 def load_sdf_grid(path: str):
