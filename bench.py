@@ -68,7 +68,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--workload", default="stanford-bunny.obj")
-    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
+                    help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
+    ap.add_argument("--group", type=int, default=8,
+                    help="N>1: frames per launch and per completion signal / gather")
+    ap.add_argument("--depth", type=int, default=3, help="N>1: groups whose slots are in flight")
+    ap.add_argument("--streams", type=int, default=2, help="N>1: HIP streams the group launches alternate over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
@@ -94,139 +100,85 @@ def frame_params(n_frames):
             for k in range(n_frames)]
 
 
-def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG, inflight=2):
-    """N=1: full frames, render kernel only. Frame k is issued on stream
-    k % inflight with its own framebuffer, so up to `inflight` independent
-    frames of the orbit are in flight: the next frame's tiles fill the GPU
-    while the previous frame's last (grazing-ray) tiles finish. inflight=1 is
-    one frame at a time. HIP events bracket each launch on its own stream.
-    Returns (wall_s, kernel_ms_avg, buffers of the last frame)."""
+def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG, inflight=2, tile=None, batch=1):
+    """N=1: full frames, render kernel only. Frames go out in launches of
+    `batch` frames (rt_render_device_frames: blockIdx.z = frame, so a frame's
+    silhouette tail is covered by the next frames' tiles); launch j is issued
+    on stream j % inflight with its own framebuffers, so up to `inflight`
+    launches are in flight. batch=1, inflight=1 is one frame at a time. HIP
+    events bracket each launch on its own stream.
+    Returns (wall_s, kernel_ms_avg per launch, buffers of the last frame)."""
     dev = torch.device("cuda")
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(inflight - 1)]
-    bufs = [(torch.empty((H, W), dtype=torch.int32, device=dev),
-             torch.empty((H, W), dtype=torch.float32, device=dev)) for _ in range(inflight)]
+    bufs = [[(torch.empty((H, W), dtype=torch.int32, device=dev),
+              torch.empty((H, W), dtype=torch.float32, device=dev)) for _ in range(batch)]
+            for _ in range(inflight)]
 
-    def issue(k, ev=None):
-        st = streams[k % inflight]
-        c, t = bufs[k % inflight]
+    def issue(j, k0, n, ev=None):
+        st = streams[j % inflight]
+        fb = bufs[j % inflight][:n]
         with torch.cuda.stream(st):
             if ev:
                 ev[0].record(st)
-            scene.render_device(params[k], c.data_ptr(), t.data_ptr(), W, H, clear=True,
-                                stream=st.cuda_stream)
+            if n == 1:
+                scene.render_device(params[k0], fb[0][0].data_ptr(), fb[0][1].data_ptr(), W, H, clear=True,
+                                    tile=tile, stream=st.cuda_stream)
+            else:
+                scene.render_device_frames(params[k0:k0 + n], [c.data_ptr() for c, _ in fb],
+                                           [t.data_ptr() for _, t in fb], W, H, rtamd.RT_FLAG_CLEAR,
+                                           tile=tile, stream=st.cuda_stream)
             if ev:
                 ev[1].record(st)
 
-    for k in range(warmup):
-        issue(k)
+    def launches(k0, nframes):
+        return [(k0 + i, min(batch, nframes - i)) for i in range(0, nframes, batch)]
+
+    for j, (k, n) in enumerate(launches(0, warmup)):
+        issue(j, k, n)
+    timed = launches(warmup, steps)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
+           for _ in timed]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        issue(warmup + k, evs[k])
+    for j, (k, n) in enumerate(timed):
+        issue(j, k, n, evs[j])
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kms = sum(a.elapsed_time(b) for a, b in evs) / steps
-    return wall, kms, bufs[(warmup + steps - 1) % inflight]
+    kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    jl, (kl, nl) = len(timed) - 1, timed[-1]
+    return wall, kms, bufs[jl % inflight][nl - 1]
 
 
-def run_distributed(scene, params, warmup, steps, rank, world, band, nslots=2):
-    """N>1: row bands per rank + one RCCL gather per frame to rank 0.
-    With the gloo backend (RTAMD_DIST_BACKEND=gloo: several ranks sharing one
-    GPU, for testing the protocol on a 1-GPU box) the packed bands are staged
-    through host memory and gathered synchronously."""
-    dev = torch.device("cuda", torch.cuda.current_device())
-    staged = dist.get_backend() == "gloo"
-    tiles = [rtamd.Tile(band, r, world, 0) for r in range(world)]
-    per = max(rtamd.lib().rt_tile_pixels(W_IMG, H_IMG, ctypes.byref(t)) for t in tiles)
-    # packed slot: [colour (per) | t (per)] as int32 words, double-buffered; rank 0
-    # gathers straight into rank-major rows of one [world, 2*per] buffer per slot
-    bufs = [torch.zeros(2 * per, dtype=torch.int32, device=dev) for _ in range(nslots)]
-    stacked = ([torch.empty((world, 2 * per), dtype=torch.int32, device=dev) for _ in range(nslots)]
-               if rank == 0 else None)
-    recv = [list(stacked[s].unbind(0)) for s in range(nslots)] if rank == 0 else None
-    # rank 0: one untiled frame per slot (the two slots' untiles run on different streams)
-    frame_c = [torch.empty((H_IMG, W_IMG), dtype=torch.int32, device=dev) for _ in range(nslots)] \
-        if rank == 0 else None
-    frame_t = [torch.empty((H_IMG, W_IMG), dtype=torch.float32, device=dev) for _ in range(nslots)] \
-        if rank == 0 else None
-    tile = tiles[rank]
-    ev = []
-
-    def untile(slot):
-        # rank r's colour words start at r*(2*per), its t words per words later
-        base = stacked[slot].data_ptr()
-        rtamd._lib.check(rtamd.lib().rt_untile_device(
-            ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * per), 2 * per,
-            ctypes.c_void_p(frame_c[slot].data_ptr()), ctypes.c_void_p(frame_t[slot].data_ptr()), W_IMG, H_IMG,
-            ctypes.byref(tiles[0]), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
-
-    # slot s = frame k % nslots: its own stream, packed buffer and gather target
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslots - 1)]
-
-    def finish(slot):
-        # the slot's previous gather must land before its buffers are reused
-        pending[slot].wait()
-        if rank == 0:
-            untile(slot)
-        pending[slot] = None
-
-    def step(k, timed):
-        last[0] = k
-        slot = k % nslots
-        b = bufs[slot]
-        with torch.cuda.stream(streams[slot]):
-            if pending[slot] is not None:
-                finish(slot)
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            scene.render_device(params[k], b.data_ptr(), b.data_ptr() + 4 * per, W_IMG, H_IMG,
-                                clear=True, tile=tile, stream=streams[slot].cuda_stream)
-            if timed:
-                e1.record()
-                ev.append((e0, e1))
-            if staged:
-                host = b.cpu()
-                lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
-                dist.gather(host, gather_list=lst, dst=0)
-                if rank == 0:
-                    stacked[slot].copy_(torch.stack(lst))
-                    untile(slot)
-                return
-            pending[slot] = dist.gather(b, gather_list=recv[slot] if rank == 0 else None, dst=0,
-                                        async_op=True)
-
-    def drain():
-        # oldest first, so the frame left in frame_c/frame_t is the last one rendered
-        for j in range(nslots - 1, -1, -1):
-            slot = (last[0] - j) % nslots
-            if pending[slot] is not None:
-                with torch.cuda.stream(streams[slot]):
-                    finish(slot)
-
-    pending = [None] * nslots
-    last = [0]
-    for k in range(warmup):
-        step(k, False)
-    drain()
-    torch.cuda.synchronize()
+def run_distributed(scene, params, warmup, steps, a):
+    """N>1: row bands per rank, assembled on rank 0 (rtamd.rowsplit). With the
+    p2p exchange every rank stores its hit pixels straight into rank 0's frame
+    over xGMI and one 4-byte RCCL all-reduce per group of frames signals
+    completion; with the gather exchange one RCCL gather per group moves the
+    packed bands (8 B/pixel). With the gloo backend (RTAMD_DIST_BACKEND=gloo:
+    several ranks sharing one GPU, a protocol test on a 1-GPU box) signals and
+    gathers are host-synchronous."""
+    from rtamd.rowsplit import RowSplitRenderer
+    rs = RowSplitRenderer(scene, W_IMG, H_IMG, band_rows=a.band_rows, group=a.group, depth=a.depth,
+                          streams=a.streams, exchange=a.exchange)
+    rs.render(params[:warmup])
+    rs.drain()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        step(warmup + k, True)
-    drain()
-    torch.cuda.synchronize()
+    rs.render(params[warmup:warmup + steps])
+    rs.host_issue_s = time.perf_counter() - t0  # host time to issue every launch and signal
+    rs.drain()
     dist.barrier()
     wall = time.perf_counter() - t0
-    kms = sum(a.elapsed_time(b) for a, b in ev) / steps
-    ls = last[0] % nslots
-    return wall, kms, tile, (frame_c[ls], frame_t[ls]) if rank == 0 else (None, None)
+    # render-launch duration of this rank's bands: the same launches (a.group frames each,
+    # a.streams streams) rendered locally, HIP events on each launch's stream
+    n = min(steps, 64)
+    _, kms, _ = run_single(scene, params[warmup:warmup + n], 0, n, inflight=a.streams, tile=rs.tile,
+                           batch=a.group)
+    return wall, kms, rs
 
 
-def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None):
+def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None, frames_per_launch=1):
     """Algorithmic bytes per launch (SURVEY.md 8(d) byte model, counted exactly
     by the counting variant of the kernel over the same frames) / the kernel's
     event-timed average launch duration over the timed region (kernel_ms, what
@@ -234,13 +186,15 @@ def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None):
     overlap; the amortized rate (wall / launches) is reported beside it."""
     c = scene.count_work(params, W, H, clear=True, tile=tile)
     npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
-    algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params)
+    algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params) * frames_per_launch
+    if amortized_ms is not None:
+        amortized_ms *= frames_per_launch
     achieved = algo / (kms * 1e-3) / 1e9
     per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
            "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
-           "work_per_ray": per_ray}
+           "work_per_ray": per_ray, "frames_per_launch": frames_per_launch}
     if amortized_ms is not None:
         # launches overlap (frames in flight): algorithmic bytes per amortized launch.
         # The byte model counts cache-served bytes, so this can exceed the HBM peak.
@@ -423,18 +377,21 @@ def main():
             latency = {"ms_per_frame": round(lwall * 1e3 / min(a.steps, 64), 4),
                        "kernel_ms": round(lkms, 5)}
     else:
-        wall, kms, tile, frame = run_distributed(scene, params, a.warmup, a.steps, rank, world,
-                                                 a.band_rows, max(2, a.inflight))
+        wall, kms, rs = run_distributed(scene, params, a.warmup, a.steps, a)
+        tile = rs.tile
         t = torch.tensor([wall], dtype=torch.float64,
                          device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-        if rank == 0:  # the gathered last frame must equal a whole-frame render of it
+        if rank == 0:  # the assembled last frame must equal a whole-frame render of it
             _, _, (c1, t1) = run_single(scene, params[-1:], 0, 1, inflight=1)
-            check_equal = bool(torch.equal(c1, frame[0]) and torch.equal(t1.view(torch.int32),
-                                                                         frame[1].view(torch.int32)))
+            fc, ft = rs.last()
+            check_equal = bool(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
+        dist.barrier()
+        rs.close()
 
-    rl = roofline(scene, params[a.warmup:], tile, kms, amortized_ms=wall * 1e3 / a.steps)
+    rl = roofline(scene, params[a.warmup:], tile, kms, amortized_ms=wall * 1e3 / a.steps,
+                  frames_per_launch=a.group if use_dist else 1)
     if pmc is not None:
         rl["traffic"] = None if pmc[0] is None else round(pmc[0])
         rl["traffic_detail"] = pmc[1]
@@ -448,16 +405,18 @@ def main():
         "config": {"workload": f"{a.workload} triangles {W_IMG}x{H_IMG} primary rays "
                                "(BASELINE configs[1]); Normal shading, no plane",
                    "resolution": [W_IMG, H_IMG], "camera": "orbit r=2.5 h=0.5 fovy 45",
-                   "parallelism": f"row bands of {a.band_rows} rows x {world} GPUs + RCCL gather"
+                   "parallelism": (f"row bands of {a.band_rows} rows x {world} GPUs, exchange "
+                                   f"{rs.exchange}, {a.group} frames per launch and signal, {a.streams} streams")
                    if use_dist else "1 GPU, 1 thread per pixel",
-                   "frames_in_flight": a.inflight},
+                   "frames_in_flight": a.inflight if not use_dist else a.group * a.streams},
         "roofline": rl,
     }
     if latency is not None:
         out["frame_latency"] = latency
     if use_dist and rank == 0:
-        out["frame_check"] = {"gathered_equals_single_render": check_equal,
-                              "backend": dist.get_backend()}
+        out["frame_check"] = {"assembled_equals_single_render": check_equal,
+                              "backend": dist.get_backend(), "exchange": rs.exchange}
+        out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_extra:
         out["extra"] = run_extras(min(a.warmup, 8), min(a.steps, 64), a.inflight)
     if rank == 0 and not use_dist and not a.no_cpu_baseline:

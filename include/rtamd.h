@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 2
+#define RTAMD_ABI_VERSION 3
 
 enum rt_status {
   RT_OK = 0,
@@ -46,6 +46,12 @@ enum rt_scene_kind { RT_SCENE_MESH = 1, RT_SCENE_GRID = 2, RT_SCENE_OCTREE = 3 }
                             src/raytracing.hpp:16-19) and write every pixel: clear+draw fused.
                             Without it, t is read as tPrev and color/t are written only on hit
                             (src/raytracing.cpp:89-94). */
+#define RT_FLAG_TILE_NATURAL 2u /* with a tile: write this rank's bands at their own rows of a
+                                   full W*H frame (e.g. rank 0's frame mapped over xGMI by
+                                   rt_ipc_open) instead of packed */
+#define RT_FLAG_HITS_ONLY 4u /* with RT_FLAG_CLEAR: the frame is already cleared (rt_clear_device),
+                                so only hit pixels are stored -- the same image as CLEAR alone,
+                                with misses costing no stores (no xGMI traffic for background) */
 
 typedef struct rt_scene rt_scene; /* opaque: owns the device copy of one scene on one GPU */
 typedef struct rt_sdf_mesh rt_sdf_mesh; /* opaque: a triangle mesh prepared for SDF queries */
@@ -151,6 +157,33 @@ int rt_untile_device(const uint32_t *d_packed_color, const float *d_packed_t, in
                      void *stream);
 /* Pixels a rank owns under `tile` (its packed buffer length). */
 int64_t rt_tile_pixels(int32_t W, int32_t H, const rt_tile *tile);
+/* rt_render_device for `frames` frames of one size/tile/shading path, on
+ * `stream`: frame f uses params[f], d_color[f], d_t[f]. Up to 8 frames share
+ * ONE launch (blockIdx.z = frame), so each frame's silhouette tail is covered
+ * by the next frames' tiles; the image of every frame is identical to
+ * rt_render_device's. */
+int rt_render_device_frames(rt_scene *s, const rt_render_params *params, int32_t frames,
+                            uint32_t *const *d_color, float *const *d_t, int32_t W, int32_t H,
+                            uint32_t flags, const rt_tile *tile, void *stream);
+/* FrameBuffer::clear() (src/raytracing.hpp:16-19) on device buffers: color = 0,
+ * t = +inf over n pixels, on `stream`. */
+int rt_clear_device(uint32_t *d_color, float *d_t, int64_t n, void *stream);
+
+/* ---- frame exchange over xGMI (multi-GPU, one process per GPU) -----------
+ * Rank 0 allocates its frame slots with rt_exchange_alloc, exports them with
+ * rt_ipc_get_handle, and every other rank maps them with rt_ipc_open; the ranks
+ * then render their bands straight into rank 0's frame (RT_FLAG_TILE_NATURAL |
+ * RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY). Slots are uncached device memory, so
+ * peer stores land where rank 0's kernels read them. Replaces the reference's
+ * framebuffer (src/raytracing.hpp:9-20) for the row-split render. */
+#define RT_IPC_HANDLE_BYTES 64
+int rt_exchange_alloc(int64_t bytes, void **d_ptr);
+int rt_exchange_free(void *d_ptr);
+int rt_ipc_get_handle(void *d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]);
+/* Map a peer's exported allocation on the current device; *d_ptr is usable by
+ * kernels of this device (peer access over xGMI). */
+int rt_ipc_open(const uint8_t handle[RT_IPC_HANDLE_BYTES], void **d_ptr);
+int rt_ipc_close(void *d_ptr);
 
 /* ---- rays (IScene::intersect) ------------------------------------------- */
 /* Batch of n rays, host buffers. hit[i] (0/1), t[i], normal[3i..3i+2] exactly

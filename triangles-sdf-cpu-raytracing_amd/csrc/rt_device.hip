@@ -275,9 +275,8 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 // 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
 
 template <class S, int SLOTS, bool GENERAL, int DIAG>
-__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
-                                                        unsigned long long *counters) {
-  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+__device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
+                                            unsigned long long *counters, uint32_t *stk) {
   typename CntSel<DIAG>::T cnt{};
   unsigned long long t_start = 0;
   if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
@@ -301,8 +300,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
     const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
     const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
     const f3 d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
-    const size_t idx = active ? (size_t)yl * fa.W + xo : 0;
+    // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
+    // full frame's own row (a peer's frame mapped over xGMI)
+    const int yb = (fa.flags & RT_FLAG_TILE_NATURAL) ? yo : yl;
+    const size_t idx = active ? (size_t)yb * fa.W + xo : 0;
     const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
+    const bool hits_only = (fa.flags & RT_FLAG_HITS_ONLY) != 0;
     const float tPrev = (clear || !active) ? kInf : fa.t[idx];
     const float tFarEff = std_min(100.0f, tPrev);  // std::min(tFar, tPrev)
     bool hit;
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
     const bool store = hit && !__builtin_isinf(t);
     if (!active) {
       // helper lane of the cooperative path: no pixel of its own
-    } else if (clear) {
+    } else if (clear && !hits_only) {
       fb_store(fa.color + idx, store ? pack_rgba(c) : 0u);
       fb_store(fa.t + idx, store ? t : kInf);
     } else if (store) {
@@ -380,6 +383,29 @@ __global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, Frame
   }
 }
 
+template <class S, int SLOTS, bool GENERAL, int DIAG>
+__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
+                                                        unsigned long long *counters) {
+  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  render_body<S, SLOTS, GENERAL, DIAG>(sc, pl, fa, counters, stk);
+}
+
+// Several frames in one launch: blockIdx.z selects the frame. The tiles of
+// frame z+1 fill the CUs while frame z's last tiles (grazing rays at the
+// silhouette, the per-frame tail) finish, so only the batch's last frame
+// leaves a tail. The per-frame arguments travel in the kernarg segment
+// (uniform blockIdx.z index: scalar loads).
+constexpr int kMaxBatch = 8;
+struct FrameBatch {
+  FrameArgs f[kMaxBatch];
+};
+
+template <class S, int SLOTS, bool GENERAL>
+__global__ __launch_bounds__(kBlock) void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
+  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  render_body<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[blockIdx.z], nullptr, stk);
+}
+
 template <class S, int SLOTS>
 __global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const float *o3,
                                                        const float *d3, int64_t n, float tn,
@@ -399,6 +425,20 @@ __global__ __launch_bounds__(kBlock) void rays_kernel(S sc, PlaneDev pl, const f
   nrm[3 * i + 1] = sh.h.n.y;
   nrm[3 * i + 2] = sh.h.n.z;
   prim[i] = sh.h.hit ? sh.h.prim : -1;
+}
+
+// FrameBuffer::clear() (raytracing.hpp:16-19): 16 B per lane per buffer.
+__global__ void clear_kernel(uint32_t *c, float *t, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    *reinterpret_cast<uint4 *>(c + i) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<float4 *>(t + i) = make_float4(kInf, kInf, kInf, kInf);
+  } else {
+    for (int64_t j = i; j < n; ++j) {
+      c[j] = 0u;
+      t[j] = kInf;
+    }
+  }
 }
 
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
@@ -672,6 +712,51 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
   return RT_OK;
 }
 
+template <class S, int MAXD>
+void launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
+                    hipStream_t stream) {
+  const dim3 grid((fb.f[0].W + kTile - 1) / kTile, (fb.f[0].rows_local + kTile - 1) / kTile, n);
+  if (general)
+    render_batch_kernel<S, MAXD, true><<<grid, kBlock, 0, stream>>>(sc, pl, fb);
+  else
+    render_batch_kernel<S, MAXD, false><<<grid, kBlock, 0, stream>>>(sc, pl, fb);
+}
+
+// One launch for n <= kMaxBatch frames of equal size / tile (blockIdx order).
+int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
+  const bool general = s->plane.on || fb.f[0].P.shading_mode != RT_SHADING_NORMAL;
+  for (int i = 0; i < n; ++i) {
+    if (general != (s->plane.on || fb.f[i].P.shading_mode != RT_SHADING_NORMAL))
+      return set_err(RT_E_INVALID, "frames of one batch must share the shading path");
+    fb.f[i].order = nullptr;
+    fb.f[i].cost = nullptr;
+  }
+  if (s->kind == RT_SCENE_MESH) {
+    MeshS sc{mesh_dev(s)};
+    switch (s->maxd) {
+      case 4: launch_batch_t<MeshS, 4>(sc, s->plane, fb, n, general, stream); break;
+      case 7: launch_batch_t<MeshS, 7>(sc, s->plane, fb, n, general, stream); break;
+      case 15: launch_batch_t<MeshS, 15>(sc, s->plane, fb, n, general, stream); break;
+      default: launch_batch_t<MeshS, 31>(sc, s->plane, fb, n, general, stream); break;
+    }
+  } else if (s->kind == RT_SCENE_GRID) {
+    GridS sc{grid_dev(s)};
+    launch_batch_t<GridS, 1>(sc, s->plane, fb, n, general, stream);
+  } else if (s->kind == RT_SCENE_OCTREE) {
+    OctS sc{OctDev{s->d_child, s->d_ovals}};
+    switch (s->maxd) {
+      case 4: launch_batch_t<OctS, 4>(sc, s->plane, fb, n, general, stream); break;
+      case 7: launch_batch_t<OctS, 7>(sc, s->plane, fb, n, general, stream); break;
+      case 15: launch_batch_t<OctS, 15>(sc, s->plane, fb, n, general, stream); break;
+      default: launch_batch_t<OctS, 31>(sc, s->plane, fb, n, general, stream); break;
+    }
+  } else {
+    return set_err(RT_E_STATE, "scene has no geometry");
+  }
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
 int check_params(const rt_render_params *p, int32_t W, int32_t H) {
   if (!p) return set_err(RT_E_INVALID, "params is NULL");
   if (W <= 0 || H <= 0 || (int64_t)W * H > (int64_t)1 << 31) return set_err(RT_E_INVALID, "bad frame size");
@@ -691,6 +776,10 @@ int fill_frame(FrameArgs &fa, const rt_render_params *p, uint32_t *c, float *t, 
   fa.rank = 0;
   fa.nranks = 1;
   fa.rows_local = H;
+  if ((flags & RT_FLAG_HITS_ONLY) && !(flags & RT_FLAG_CLEAR))
+    return set_err(RT_E_INVALID, "RT_FLAG_HITS_ONLY needs RT_FLAG_CLEAR (a cleared frame)");
+  if (flags & ~(RT_FLAG_CLEAR | RT_FLAG_TILE_NATURAL | RT_FLAG_HITS_ONLY))
+    return set_err(RT_E_INVALID, "unknown render flag");
   if (tile && tile->num_ranks > 1) {
     if (tile->band_rows <= 0 || tile->rank < 0 || tile->rank >= tile->num_ranks)
       return set_err(RT_E_INVALID, "bad tile");
@@ -973,6 +1062,75 @@ int rt_render_device(rt_scene *s, const rt_render_params *p, uint32_t *d_color, 
   if ((rc = fill_frame(fa, p, d_color, d_t, W, H, flags, tile))) return rc;
   if (fa.rows_local <= 0) return RT_OK;
   return launch_render(s, fa, (hipStream_t)stream);
+}
+
+int rt_render_device_frames(rt_scene *s, const rt_render_params *params, int32_t frames,
+                            uint32_t *const *d_color, float *const *d_t, int32_t W, int32_t H,
+                            uint32_t flags, const rt_tile *tile, void *stream) {
+  if (!s || !params || !d_color || !d_t || frames < 0) return set_err(RT_E_INVALID, "bad arguments");
+  if (frames == 1) return rt_render_device(s, params, d_color[0], d_t[0], W, H, flags, tile, stream);
+  FrameBatch fb;
+  for (int32_t f0 = 0; f0 < frames; f0 += kMaxBatch) {
+    const int n = std::min<int32_t>(kMaxBatch, frames - f0);
+    for (int i = 0; i < n; ++i) {
+      int rc = check_params(params + f0 + i, W, H);
+      if (rc) return rc;
+      if (!d_color[f0 + i] || !d_t[f0 + i]) return set_err(RT_E_INVALID, "NULL framebuffer");
+      if ((rc = fill_frame(fb.f[i], params + f0 + i, d_color[f0 + i], d_t[f0 + i], W, H, flags, tile)))
+        return rc;
+    }
+    if (fb.f[0].rows_local <= 0) return RT_OK;
+    const int rc = launch_batch(s, fb, n, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return RT_OK;
+}
+
+int rt_clear_device(uint32_t *d_color, float *d_t, int64_t n, void *stream) {
+  if (!d_color || !d_t || n < 0) return set_err(RT_E_INVALID, "bad arguments");
+  if (((uintptr_t)d_color | (uintptr_t)d_t) & 15) return set_err(RT_E_INVALID, "buffers must be 16-byte aligned");
+  if (n == 0) return RT_OK;
+  const int64_t lanes = (n + 3) / 4;
+  clear_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, (hipStream_t)stream>>>(d_color, d_t, n);
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+// Exchange slots: uncached device memory, so stores arriving from a peer GPU
+// over xGMI are never shadowed by stale lines in this GPU's L2.
+int rt_exchange_alloc(int64_t bytes, void **d_ptr) {
+  if (!d_ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad arguments");
+  *d_ptr = nullptr;
+  HIP_TRY(hipExtMallocWithFlags(d_ptr, (size_t)bytes, hipDeviceMallocUncached));
+  return RT_OK;
+}
+
+int rt_exchange_free(void *d_ptr) {
+  if (d_ptr) HIP_TRY(hipFree(d_ptr));
+  return RT_OK;
+}
+
+int rt_ipc_get_handle(void *d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]) {
+  static_assert(sizeof(hipIpcMemHandle_t) == RT_IPC_HANDLE_BYTES, "IPC handle size");
+  if (!d_ptr || !handle) return set_err(RT_E_INVALID, "bad arguments");
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, d_ptr));
+  std::memcpy(handle, &h, sizeof h);
+  return RT_OK;
+}
+
+int rt_ipc_open(const uint8_t handle[RT_IPC_HANDLE_BYTES], void **d_ptr) {
+  if (!d_ptr || !handle) return set_err(RT_E_INVALID, "bad arguments");
+  *d_ptr = nullptr;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  HIP_TRY(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return RT_OK;
+}
+
+int rt_ipc_close(void *d_ptr) {
+  if (d_ptr) HIP_TRY(hipIpcCloseMemHandle(d_ptr));
+  return RT_OK;
 }
 
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,

@@ -15,6 +15,9 @@ LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(PKG_ROOT, "lib", "librtam
 
 RT_OK = 0
 RT_FLAG_CLEAR = 1
+RT_FLAG_TILE_NATURAL = 2
+RT_FLAG_HITS_ONLY = 4
+RT_IPC_HANDLE_BYTES = 64
 RT_SCENE_MESH, RT_SCENE_GRID, RT_SCENE_OCTREE = 1, 2, 3
 
 _lib = None
@@ -81,6 +84,14 @@ _SIGS = {
     "rt_untile_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_tile_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_void_p]),
+    "rt_render_device_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                          C.c_int32, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "rt_clear_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "rt_exchange_alloc": (C.c_int, [C.c_int64, C.POINTER(C.c_void_p)]),
+    "rt_exchange_free": (C.c_int, [C.c_void_p]),
+    "rt_ipc_get_handle": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_ipc_open": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "rt_ipc_close": (C.c_int, [C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_float,
                                     C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_count_work": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,

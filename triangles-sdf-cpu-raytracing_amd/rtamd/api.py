@@ -271,12 +271,25 @@ class IScene:
         return ms.value
 
     def render_device(self, params: RenderParams, color_ptr: int, t_ptr: int, W: int, H: int,
-                      clear: bool = True, tile: Tile | None = None, stream: int | None = None):
-        """Renderer::draw into device buffers (e.g. torch tensors' data_ptr())."""
+                      clear: bool = True, tile: Tile | None = None, stream: int | None = None,
+                      flags: int = 0):
+        """Renderer::draw into device buffers (e.g. torch tensors' data_ptr()).
+        `flags` adds RT_FLAG_TILE_NATURAL / RT_FLAG_HITS_ONLY (include/rtamd.h)."""
         check(lib().rt_render_device(self._handle(), C.byref(params), C.c_void_p(color_ptr),
-                                     C.c_void_p(t_ptr), W, H, RT_FLAG_CLEAR if clear else 0,
+                                     C.c_void_p(t_ptr), W, H, (RT_FLAG_CLEAR if clear else 0) | flags,
                                      C.byref(tile) if tile is not None else None,
                                      C.c_void_p(stream) if stream else None))
+
+    def render_device_frames(self, params_list, color_ptrs, t_ptrs, W: int, H: int, flags: int,
+                             tile: Tile | None = None, stream: int | None = None):
+        """rt_render_device_frames: one launch per frame, one host call."""
+        n = len(params_list)
+        arr = (RenderParams * n)(*params_list)
+        cp = (C.c_void_p * n)(*color_ptrs)
+        tp = (C.c_void_p * n)(*t_ptrs)
+        check(lib().rt_render_device_frames(self._handle(), arr, n, cp, tp, W, H, flags,
+                                            C.byref(tile) if tile is not None else None,
+                                            C.c_void_p(stream) if stream else None))
 
     def bench_frames(self, params_list, W: int, H: int, clear: bool = True):
         arr = (RenderParams * len(params_list))(*params_list)
