@@ -5,28 +5,32 @@ Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355
 Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
 1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
 the pure intersection hot path), over a deterministic 64-frame camera orbit
-(SURVEY.md 8(d)). A "step" is one frame. The orbit's frames are independent,
-so --inflight (default 3, triple buffering) of them are in flight at once, each on its own HIP
-stream and framebuffer: the next frame's tiles fill the GPU while the previous
-frame's last tiles (grazing rays at the silhouette, the per-frame tail)
-finish. value = rays of all K frames / wall time of the K frames; the
-one-frame-at-a-time latency is reported beside it ("frame_latency"). At N=1 the other BASELINE configs
-are measured the same way and reported under "extra" (rank 0): the SDF grid
-(configs[2]) on a 256^3 SDF of stanford-bunny generated on the GPU (stand-in:
-example_grid_large.grid is missing from the reference) and on the shipped
-65^3 example_grid.grid; the octree (configs[3]) at 3840x2160 on a depth-8
-generated octree (stand-in for example_octree_large.octree) and on the
-shipped sdf_6.octree; and the config-5 mesh stand-in (stanford-bunny
-subdivided twice, 1,111,216 triangles) at 3840x2160.
+(SURVEY.md 8(d)). A "step" is one frame. The orbit's frames are independent:
+--group (default 8) of them go out in ONE launch (blockIdx.z = frame), so a
+frame's last tiles (grazing rays at the silhouette, the per-frame tail) are
+covered by the next frames' tiles, and launches alternate over --streams
+(default 2) HIP streams with their own framebuffers, so one launch's tail
+overlaps the next launch. value = rays of all K frames / wall time of the K
+frames; the one-frame-at-a-time latency is reported beside it
+("frame_latency"). At N=1 the other BASELINE configs are measured the same way
+and reported under "extra" (rank 0): the SDF grid (configs[2]) on a 256^3 SDF
+of stanford-bunny generated on the GPU (stand-in: example_grid_large.grid is
+missing from the reference) and on the shipped 65^3 example_grid.grid; the
+octree (configs[3]) at 3840x2160 on a depth-8 generated octree (stand-in for
+example_octree_large.octree) and on the shipped sdf_6.octree; and the config-5
+mesh stand-in (stanford-bunny subdivided twice, 1,111,216 triangles) at
+3840x2160.
 
-Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every frame is
-split into 16-row bands dealt round-robin to the ranks (load balance: the model
-covers the middle rows); each rank renders its bands packed, then ONE RCCL
-gather per frame brings colour+t (8 B/pixel) to rank 0, which de-interleaves
-them on the device. Frames rotate over max(2, --inflight) streams with their
-own packed buffers, so frame k's gather (and its untile on rank 0) overlaps
-the next frames' renders. Total work per step is fixed (one 1080p frame), so scaling
-is "strong"; value = pixels of all frames / max-over-ranks wall time.
+Multi-GPU (torch.distributed.run, one process per GPU; rtamd.rowsplit): every
+frame is split into --band-rows (8) row bands dealt round-robin to the ranks
+(load balance: the model covers the middle rows), with the same launches
+(--group frames, --streams streams). Exchange p2p (default): each rank's
+kernel stores its HIT pixels straight into rank 0's frame slots over xGMI
+(IPC-mapped), and one 4-byte RCCL all-reduce per group signals completion;
+exchange gather: one RCCL gather per group of the packed bands (8 B/pixel) and
+a de-interleave on rank 0. Total work per step is fixed (one 1080p frame), so
+scaling is "strong"; value = pixels of all frames / max-over-ranks wall time.
+rank 0 checks that its last assembled frame equals a whole-frame render.
 
 Timing: W untimed warm-up frames, then exactly K frames between barrier +
 torch.cuda.synchronize() on both sides; max over ranks. Inputs are resident
@@ -72,15 +76,13 @@ def parse():
     ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
                     help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
     ap.add_argument("--group", type=int, default=8,
-                    help="N>1: frames per launch and per completion signal / gather")
+                    help="frames per launch (blockIdx.z = frame); N>1: also per completion signal / gather")
     ap.add_argument("--depth", type=int, default=3, help="N>1: groups whose slots are in flight")
-    ap.add_argument("--streams", type=int, default=2, help="N>1: HIP streams the group launches alternate over")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams the launches alternate over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="orbit frames in flight (one HIP stream each); 1 = one frame at a time")
     ap.add_argument("--dist", action="store_true",
                     help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
@@ -278,7 +280,7 @@ EXTRAS = [
 ]
 
 
-def run_extras(warmup, steps, inflight):
+def run_extras(warmup, steps, streams, group):
     out = {}
     for key, src, W, H, desc in EXTRAS:
         if "." in src:
@@ -289,11 +291,11 @@ def run_extras(warmup, steps, inflight):
         sc.set_plane(None)
         orbit = WL.orbit_positions(64)
         prm = [WL.params_for(orbit[k % 64], W, H, rtamd.ShadingMode.Normal) for k in range(warmup + steps)]
-        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H, inflight)
+        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H, inflight=streams, batch=group)
         out[key] = {"workload": f"{desc}, {W}x{H} primary rays, same orbit",
                     "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
                     "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
-                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps)}
+                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps, group)}
         sc.close()
         torch.cuda.synchronize()
     return out
@@ -370,9 +372,9 @@ def main():
 
     latency = None
     if not use_dist:
-        wall, kms, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.inflight)
+        wall, kms, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.streams, batch=a.group)
         tile = None
-        if a.inflight > 1:  # single-frame latency (one frame at a time), reported beside
+        if a.streams * a.group > 1:  # single-frame latency (one frame at a time), reported beside
             lwall, lkms, _ = run_single(scene, params, min(a.warmup, 8), min(a.steps, 64), inflight=1)
             latency = {"ms_per_frame": round(lwall * 1e3 / min(a.steps, 64), 4),
                        "kernel_ms": round(lkms, 5)}
@@ -391,7 +393,7 @@ def main():
         rs.close()
 
     rl = roofline(scene, params[a.warmup:], tile, kms, amortized_ms=wall * 1e3 / a.steps,
-                  frames_per_launch=a.group if use_dist else 1)
+                  frames_per_launch=a.group)
     if pmc is not None:
         rl["traffic"] = None if pmc[0] is None else round(pmc[0])
         rl["traffic_detail"] = pmc[1]
@@ -408,7 +410,7 @@ def main():
                    "parallelism": (f"row bands of {a.band_rows} rows x {world} GPUs, exchange "
                                    f"{rs.exchange}, {a.group} frames per launch and signal, {a.streams} streams")
                    if use_dist else "1 GPU, 1 thread per pixel",
-                   "frames_in_flight": a.inflight if not use_dist else a.group * a.streams},
+                   "frames_per_launch": a.group, "streams": a.streams},
         "roofline": rl,
     }
     if latency is not None:
@@ -418,7 +420,7 @@ def main():
                               "backend": dist.get_backend(), "exchange": rs.exchange}
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_extra:
-        out["extra"] = run_extras(min(a.warmup, 8), min(a.steps, 64), a.inflight)
+        out["extra"] = run_extras(min(a.warmup, 16), min(a.steps, 64), a.streams, a.group)
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:

@@ -16,7 +16,8 @@ from rtamd import workloads as WL  # noqa: E402
 
 SIZES = {"bunny": (1920, 1080), "grid": (1920, 1080), "example_grid.grid": (1920, 1080),
          "octree": (3840, 2160), "sdf_6.octree": (3840, 2160), "mesh_large": (3840, 2160)}
-VARIANTS = [(1, 1), (1, 3), (2, 2), (4, 1), (4, 2), (8, 1), (8, 2), (8, 3)]
+VARIANTS = [tuple(int(x) for x in v.split("x")) for v in
+            os.environ.get("AB_VARIANTS", "1x1,1x3,2x2,4x1,4x2,8x1,8x2,8x3").split(",")]
 
 
 def scene_for(name):

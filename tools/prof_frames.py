@@ -16,8 +16,13 @@ ap.add_argument("--W", type=int, default=1920)
 ap.add_argument("--H", type=int, default=1080)
 ap.add_argument("--mode", default="primary")
 a = ap.parse_args()
-kind, payload, off = WL.load_input(a.workload)
-s = WL.make_scene(kind, payload)
+if a.workload in ("grid", "octree", "mesh_large"):  # bench.py's generated stand-ins
+    sys.path.insert(0, ROOT)
+    import bench  # noqa: E402
+    s, off = bench.standin_scenes(a.workload), -1.0
+else:
+    kind, payload, off = WL.load_input(a.workload)
+    s = WL.make_scene(kind, payload)
 if a.mode == "primary":
     s.set_plane(None)
     P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Normal) for p in WL.orbit_positions(64)]
