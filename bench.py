@@ -160,10 +160,30 @@ def run_distributed(scene, params, warmup, steps, a):
     several ranks sharing one GPU, a protocol test on a 1-GPU box) signals and
     gathers are host-synchronous."""
     from rtamd.rowsplit import RowSplitRenderer
-    rs = RowSplitRenderer(scene, W_IMG, H_IMG, band_rows=a.band_rows, group=a.group, depth=a.depth,
-                          streams=a.streams, exchange=a.exchange)
-    rs.render(params[:warmup])
-    rs.drain()
+
+    def make(exchange):
+        r = RowSplitRenderer(scene, W_IMG, H_IMG, band_rows=a.band_rows, group=a.group, depth=a.depth,
+                             streams=a.streams, exchange=exchange)
+        r.render(params[:max(warmup, 1)])
+        r.drain()
+        return r
+
+    rs = make(a.exchange)
+    # the warm-up's last assembled frame must equal a whole-frame render on rank 0;
+    # a p2p exchange that fails this (IPC mapping, peer-store visibility) is replaced
+    # by the RCCL gather before anything is timed
+    ok = 1
+    if dist.get_rank() == 0:
+        _, _, (c1, t1) = run_single(scene, params[max(warmup, 1) - 1:max(warmup, 1)], 0, 1, inflight=1)
+        fc, ft = rs.last()
+        ok = int(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
+    if not rs._all_ok(ok):
+        if rs.exchange == "p2p":
+            rs.close()
+            rs = make("gather")
+            rs.fallback = "p2p warm-up frame differed from a whole-frame render"
+        else:
+            raise SystemExit("row-split gather: assembled warm-up frame differs from a whole-frame render")
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -205,10 +225,11 @@ def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None, fram
     return out
 
 
-def pmc_traffic(workload, W, H, frames=16):
-    """HBM bytes per launch of the headline render kernel from rocprofv3 PMC
-    counters, collected in two separate --pmc passes (FETCH_SIZE, WRITE_SIZE
-    cannot share a pass) over tools/prof_frames.py, as MI355X_MICROARCH.md's
+def pmc_traffic(workload, W, H, group, frames=32):
+    """HBM bytes per launch of the headline render kernel (launches of `group`
+    frames, the timed region's launch shape) from rocprofv3 PMC counters,
+    collected in two separate --pmc passes (FETCH_SIZE, WRITE_SIZE cannot
+    share a pass) over tools/prof_frames.py, as MI355X_MICROARCH.md's
     HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
     FETCH_SIZE reports half the bytes of coalesced reads, so it is doubled.
     Runs as child processes BEFORE this process touches the GPU. Returns
@@ -223,13 +244,15 @@ def pmc_traffic(workload, W, H, frames=16):
         return None, {"error": "rocprofv3 not found"}
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}
+    kname = "render_batch_kernel" if group > 1 else "render_kernel"
     tmp = tempfile.mkdtemp(prefix="rtamd_pmc_", dir="/tmp")
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
             cmd = ["timeout", "-k", "10", "180", prof, "--pmc", ctr, "--output-format", "csv", "-d", d,
                    "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_frames.py"),
-                   "--workload", workload, "--frames", str(frames), "--W", str(W), "--H", str(H)]
+                   "--workload", workload, "--frames", str(frames), "--W", str(W), "--H", str(H),
+                   "--group", str(group)]
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
             if r.returncode != 0:
                 return None, {"error": f"{ctr} pass rc={r.returncode}: {r.stderr[-300:]}"}
@@ -237,10 +260,10 @@ def pmc_traffic(workload, W, H, frames=16):
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if "render_kernel" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                        if kname in row["Kernel_Name"] and row["Counter_Name"] == ctr:
                             per.append(float(row["Counter_Value"]))
             if not per:
-                return None, {"error": f"no {ctr} rows for render_kernel"}
+                return None, {"error": f"no {ctr} rows for {kname}"}
             vals[ctr] = sum(per) / len(per)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -248,7 +271,8 @@ def pmc_traffic(workload, W, H, frames=16):
     write = vals["WRITE_SIZE"] * 1024.0
     return fetch + write, {"fetch_bytes": round(fetch), "write_bytes": round(write),
                            "raw_kib": {k: round(v, 1) for k, v in vals.items()},
-                           "launches": frames, "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
+                           "launches": frames // group, "frames_per_launch": group,
+                           "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
 
 
 def standin_scenes(which):
@@ -347,7 +371,7 @@ def main():
     use_dist = world > 1 or a.dist
     pmc = None
     if not use_dist and not a.no_pmc:
-        pmc = pmc_traffic(a.workload, W_IMG, H_IMG)  # child processes, before this one inits the GPU
+        pmc = pmc_traffic(a.workload, W_IMG, H_IMG, a.group)  # child processes, before this one inits the GPU
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
@@ -417,7 +441,8 @@ def main():
         out["frame_latency"] = latency
     if use_dist and rank == 0:
         out["frame_check"] = {"assembled_equals_single_render": check_equal,
-                              "backend": dist.get_backend(), "exchange": rs.exchange}
+                              "backend": dist.get_backend(), "exchange": rs.exchange,
+                              "fallback": getattr(rs, "fallback", None)}
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_extra:
         out["extra"] = run_extras(min(a.warmup, 16), min(a.steps, 64), a.streams, a.group)

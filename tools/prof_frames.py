@@ -15,6 +15,7 @@ ap.add_argument("--frames", type=int, default=16)
 ap.add_argument("--W", type=int, default=1920)
 ap.add_argument("--H", type=int, default=1080)
 ap.add_argument("--mode", default="primary")
+ap.add_argument("--group", type=int, default=1, help="frames per launch (bench.py's --group)")
 a = ap.parse_args()
 if a.workload in ("grid", "octree", "mesh_large"):  # bench.py's generated stand-ins
     sys.path.insert(0, ROOT)
@@ -29,5 +30,12 @@ if a.mode == "primary":
 else:
     s.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off))
     P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Lambert) for p in WL.orbit_positions(64)]
-mean, total = s.bench_frames([P[k % 64] for k in range(a.frames)], a.W, a.H)
-print(f"{a.workload} {a.W}x{a.H} {a.mode}: {mean:.4f} ms/frame", flush=True)
+frames = [P[k % 64] for k in range(a.frames)]
+if a.group > 1:  # the bench's launch shape: `group` frames per launch (one stream: counters are per dispatch)
+    sys.path.insert(0, ROOT)
+    import bench  # noqa: E402
+    wall, kms, _ = bench.run_single(s, frames, 0, a.frames, a.W, a.H, inflight=1, batch=a.group)
+    print(f"{a.workload} {a.W}x{a.H} {a.mode}: {kms:.4f} ms/launch of {a.group} frames", flush=True)
+else:
+    mean, total = s.bench_frames(frames, a.W, a.H)
+    print(f"{a.workload} {a.W}x{a.H} {a.mode}: {mean:.4f} ms/frame", flush=True)

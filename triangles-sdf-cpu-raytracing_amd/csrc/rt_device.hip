@@ -52,9 +52,17 @@ struct FrameArgs {
 // ---------------------------------------------------------- scene adapters --
 // kFields = LDS words per traversal frame (mesh: node, list|count, best t;
 // octree: node, list|count; grid: none).
+// occupancy floors (min_waves below), overridable for A/B builds
+#ifndef RT_GRID_WAVES
+#define RT_GRID_WAVES 1
+#endif
+#ifndef RT_OCT_WAVES
+#define RT_OCT_WAVES 6
+#endif
 struct MeshS {
   static constexpr int kFields = 3;
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
+  static constexpr int kMinWaves = 1;
   MeshDev d;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
@@ -84,6 +92,7 @@ struct MeshS {
 struct GridS {
   static constexpr int kFields = 1;
   static constexpr bool kCoop = false;
+  static constexpr int kMinWaves = RT_GRID_WAVES;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -99,6 +108,7 @@ struct GridS {
 struct OctS {
   static constexpr int kFields = 2;
   static constexpr bool kCoop = false;
+  static constexpr int kMinWaves = RT_OCT_WAVES;
   OctDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -220,14 +230,16 @@ __device__ __forceinline__ f4 shade_one(const S &sc, const PlaneDev &pl, const r
 // and never re-read by the kernel; plain stores keep every written line in the
 // XCD's 4 MiB L2 and push scene data out. Agent-scope relaxed atomic stores
 // lower to `global_store ... sc1`, which the MI355X L2 drops after writing.
-__device__ __forceinline__ void fb_store(uint32_t *p, uint32_t v) {
-#ifdef RT_PLAIN_FB_STORES
-  *p = v;
-#else
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-__device__ __forceinline__ void fb_store(float *p, float v) {
+// A peer's frame mapped over xGMI (RT_FLAG_TILE_NATURAL, the row-split p2p
+// exchange) takes system-scope stores: they write through this GPU's L2 to the
+// owner's memory whatever caching the IPC mapping got, so the kernel's
+// completion (before the stream-ordered RCCL signal) covers them.
+template <class T>
+__device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
+  if (peer) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
 #ifdef RT_PLAIN_FB_STORES
   *p = v;
 #else
@@ -302,7 +314,8 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
     const f3 d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
     // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
     // full frame's own row (a peer's frame mapped over xGMI)
-    const int yb = (fa.flags & RT_FLAG_TILE_NATURAL) ? yo : yl;
+    const bool peer = (fa.flags & RT_FLAG_TILE_NATURAL) != 0;
+    const int yb = peer ? yo : yl;
     const size_t idx = active ? (size_t)yb * fa.W + xo : 0;
     const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
     const bool hits_only = (fa.flags & RT_FLAG_HITS_ONLY) != 0;
@@ -331,11 +344,11 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
     if (!active) {
       // helper lane of the cooperative path: no pixel of its own
     } else if (clear && !hits_only) {
-      fb_store(fa.color + idx, store ? pack_rgba(c) : 0u);
-      fb_store(fa.t + idx, store ? t : kInf);
+      fb_store(fa.color + idx, store ? pack_rgba(c) : 0u, peer);
+      fb_store(fa.t + idx, store ? t : kInf, peer);
     } else if (store) {
-      fb_store(fa.color + idx, pack_rgba(c));
-      fb_store(fa.t + idx, t);
+      fb_store(fa.color + idx, pack_rgba(c), peer);
+      fb_store(fa.t + idx, t, peer);
     }
   }
   if constexpr (DIAG == 0) {
@@ -383,8 +396,19 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
   }
 }
 
+// Occupancy floor of the primary-ray kernels (waves per SIMD; 1 = the
+// compiler's choice). The octree primary kernel is register-limited to 5 waves
+// and gains ~5 % at 6 (a few spilled words outside the traversal loop); more
+// (8) or the same on the grid (64 VGPRs, spills in the march) lose 5-25 %.
+// Trees deeper than 7 slots are LDS-limited anyway.
 template <class S, int SLOTS, bool GENERAL, int DIAG>
-__global__ __launch_bounds__(kBlock) void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
+constexpr int min_waves() {
+  return (GENERAL || DIAG != 0 || SLOTS > 7) ? 1 : S::kMinWaves;
+}
+
+template <class S, int SLOTS, bool GENERAL, int DIAG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, DIAG>())))
+void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   render_body<S, SLOTS, GENERAL, DIAG>(sc, pl, fa, counters, stk);
@@ -401,7 +425,8 @@ struct FrameBatch {
 };
 
 template <class S, int SLOTS, bool GENERAL>
-__global__ __launch_bounds__(kBlock) void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
+void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   render_body<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[blockIdx.z], nullptr, stk);
 }
