@@ -89,6 +89,7 @@ struct MeshS {
     return mesh_occluded<B>(d, o, dir, tn, tf, st, cnt);
   }
 };
+template <int kMode>
 struct GridS {
   static constexpr int kFields = 1;
   static constexpr bool kCoop = false;
@@ -97,12 +98,12 @@ struct GridS {
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields>, CT &cnt) const {
-    return grid_intersect(d, o, dir, tn, tf, cnt);
+    return grid_intersect<kMode>(d, o, dir, tn, tf, cnt);
   }
   template <int B, class CT>
   __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields>, CT &cnt) const {
-    return grid_occluded(d, o, dir, tn, tf, cnt);
+    return grid_occluded<kMode>(d, o, dir, tn, tf, cnt);
   }
 };
 struct OctS {
@@ -561,6 +562,7 @@ struct rt_scene {
   // grid
   float *d_vals = nullptr;
   uint32_t size[3] = {0, 0, 0};
+  bool grid_bricked = false;  // device layout (rt_scenes.h GridDev): bricked, or the reference's linear
   // octree
   uint32_t *d_child = nullptr;
   rtl::OctVals *d_ovals = nullptr;
@@ -588,10 +590,42 @@ struct rt_scene {
 
 namespace {
 
+// bricked sample count of a grid (rt_scenes.h GridDev)
+uint64_t grid_bricked_samples(const uint32_t size[3]) {
+  return (uint64_t)grid_bricks(size[0]) * grid_bricks(size[1]) * grid_bricks(size[2]) * 64u;
+}
+
+// device samples of a grid scene (s->grid_bricked picks the layout)
+uint64_t grid_samples(const rt_scene *s) {
+  return s->grid_bricked ? grid_bricked_samples(s->size) : (uint64_t)s->size[0] * s->size[1] * s->size[2];
+}
+
 GridDev grid_dev(const rt_scene *s) {
-  const uint64_t n = (uint64_t)s->size[0] * s->size[1] * s->size[2];
-  return GridDev{s->d_vals, s->size[0], s->size[1], s->size[2], s->size[1] * s->size[2], n <= (1ull << 24),
-                 4 * n < (1ull << 31) ? (uint32_t)(4 * n) : 0u};
+  const uint64_t n = grid_samples(s);
+  // buffer loads address up to 4 GiB (32-bit offsets, num_records saturated at 2^32-1)
+  const uint32_t bytes = 4 * n <= (1ull << 32) ? (uint32_t)std::min<uint64_t>(4 * n, 0xFFFFFFFFull) : 0u;
+  if (!s->grid_bricked) return GridDev{s->d_vals, s->size[0], s->size[1], s->size[2], s->size[2],
+                                       s->size[1] * s->size[2], bytes};
+  const uint32_t ys = grid_bricks(s->size[2]) * 64u;
+  return GridDev{s->d_vals, s->size[0], s->size[1], s->size[2], ys, grid_bricks(s->size[1]) * ys, bytes};
+}
+
+int grid_mode(const rt_scene *s, const GridDev &gd) {
+  return (gd.bytes ? kGridBuf : 0) | (s->grid_bricked ? kGridBricked : 0);
+}
+
+// reference x-major values -> 4x4x4 bricks; one thread per bricked sample
+// (padding samples get 0 and are never read)
+__global__ __launch_bounds__(256) void brick_kernel(const float *__restrict__ src, float *__restrict__ dst,
+                                                    uint32_t sx, uint32_t sy, uint32_t sz, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t nby = grid_bricks(sy), nbz = grid_bricks(sz);
+  const uint32_t l = (uint32_t)(i & 63u);
+  const uint64_t b = i >> 6;
+  const uint32_t bz = (uint32_t)(b % nbz), by = (uint32_t)((b / nbz) % nby), bx = (uint32_t)(b / nbz / nby);
+  const uint32_t x = bx * 4 + (l >> 4), y = by * 4 + ((l >> 2) & 3u), z = bz * 4 + (l & 3u);
+  dst[i] = (x < sx && y < sy && z < sz) ? src[((uint64_t)x * sy + y) * sz + z] : 0.0f;
 }
 
 MeshDev mesh_dev(const rt_scene *s) {
@@ -719,8 +753,14 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
       default: launch_render_t<MeshS, 31>(sc, s->plane, fa, general, stream, counters, diag); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
-    GridS sc{grid_dev(s)};
-    launch_render_t<GridS, 1>(sc, s->plane, fa, general, stream, counters, diag);
+    const GridDev gd = grid_dev(s);
+    switch (grid_mode(s, gd)) {
+      case kGridBuf | kGridBricked:
+        launch_render_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, fa, general, stream, counters, diag);
+        break;
+      case kGridBricked: launch_render_t<GridS<kGridBricked>, 1>({gd}, s->plane, fa, general, stream, counters, diag); break;
+      default: launch_render_t<GridS<kGridBuf>, 1>({gd}, s->plane, fa, general, stream, counters, diag); break;
+    }
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
@@ -765,8 +805,14 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
       default: launch_batch_t<MeshS, 31>(sc, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
-    GridS sc{grid_dev(s)};
-    launch_batch_t<GridS, 1>(sc, s->plane, fb, n, general, stream);
+    const GridDev gd = grid_dev(s);
+    switch (grid_mode(s, gd)) {
+      case kGridBuf | kGridBricked:
+        launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream);
+        break;
+      case kGridBricked: launch_batch_t<GridS<kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream); break;
+      default: launch_batch_t<GridS<kGridBuf>, 1>({gd}, s->plane, fb, n, general, stream); break;
+    }
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
@@ -981,9 +1027,34 @@ int rt_scene_create_grid(const uint32_t size[3], const float *values, rt_scene *
   if (rc) return rc;
   s->kind = RT_SCENE_GRID;
   s->size[0] = size[0]; s->size[1] = size[1]; s->size[2] = size[2];
-  if ((rc = upload(&s->d_vals, values, (size_t)n, s->dev_bytes))) {
+  if ((uint64_t)n * 4 <= kGridLinearMaxBytes) {  // fits one XCD's L2: the reference layout
+    if ((rc = upload(&s->d_vals, values, (size_t)n, s->dev_bytes))) {
+      rt_scene_destroy(s);
+      return rc;
+    }
+    *out = s;
+    return RT_OK;
+  }
+  const uint64_t nb = grid_bricked_samples(size);
+  if (nb >= (1ull << 32)) {
+    rt_scene_destroy(s);
+    return set_err(RT_E_INVALID, "bad grid size");
+  }
+  s->grid_bricked = true;
+  float *d_ref = nullptr;  // the reference array, staged for the device-side bricking
+  if ((rc = upload(&d_ref, values, (size_t)n, s->dev_bytes)) ||
+      (rc = upload(&s->d_vals, (const float *)nullptr, (size_t)nb, s->dev_bytes))) {
+    if (d_ref) (void)hipFree(d_ref);
     rt_scene_destroy(s);
     return rc;
+  }
+  s->dev_bytes -= (int64_t)(n * sizeof(float));
+  brick_kernel<<<(unsigned)((nb + 255) / 256), 256>>>(d_ref, s->d_vals, size[0], size[1], size[2], nb);
+  const hipError_t e1 = hipGetLastError(), e2 = hipDeviceSynchronize(), e3 = hipFree(d_ref);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    rt_scene_destroy(s);
+    return set_err(RT_E_DEVICE, std::string("grid bricking: ") +
+                                    hipGetErrorString(e1 != hipSuccess ? e1 : e2 != hipSuccess ? e2 : e3));
   }
   *out = s;
   return RT_OK;
@@ -1223,8 +1294,16 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
         default: launch_rays_t<MeshS, 31>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     } else if (s->kind == RT_SCENE_GRID) {
-      GridS sc{grid_dev(s)};
-      launch_rays_t<GridS, 1>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP);
+      const GridDev gd = grid_dev(s);
+      switch (grid_mode(s, gd)) {
+        case kGridBuf | kGridBricked:
+          launch_rays_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP);
+          break;
+        case kGridBricked:
+          launch_rays_t<GridS<kGridBricked>, 1>({gd}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP);
+          break;
+        default: launch_rays_t<GridS<kGridBuf>, 1>({gd}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+      }
     } else {
       OctS sc{OctDev{s->d_child, s->d_ovals}};
       switch (s->maxd) {

@@ -612,18 +612,57 @@ __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, flo
 // ------------------------------------------------------------------- grid --
 // SDFGrid (grid_raytracing.cpp:1-125): trilinear sdf over 8 taps of an
 // x-major grid, sphere tracing inside [-1,1]^3 until sdf < 1e-3.
+//
+// Device layouts (values are the reference's, bit for bit; only addresses
+// change):
+//  - linear: the reference's x-major array, index (x*sy + y)*sz + z. Grids
+//    that fit one XCD's L2 (<= 4 MiB) keep it.
+//  - bricked: 4x4x4 bricks of 256 B (two 128 B lines), bricks x-major like
+//    the reference array, samples inside a brick (lx, ly, lz) at
+//    lx*16 + ly*4 + lz. The x-major array puts the 2x2x2 taps of one
+//    evaluation on 4 different lines (x and y neighbours are a plane / a row
+//    apart), and a wave's footprint of k^3 cells on ~k^2 mostly unused lines;
+//    a brick holds a 4^3 neighbourhood, so the same evaluations touch ~2.3
+//    lines and neighbouring lanes and steps share them (256^3 grid, 1080p:
+//    0.0646 -> 0.0507 ms per frame). The padding up to a multiple of 4 per
+//    axis is never read (taps are at most size-1).
+constexpr uint32_t kBrick = 4;
+constexpr uint64_t kGridLinearMaxBytes = 4ull << 20;
 struct GridDev {
   const float *__restrict__ v;
-  uint32_t sx, sy, sz;
-  uint32_t syz;    // sy * sz
-  bool small;      // sx * sy * sz <= 2^24: 24-bit multiplies are exact for every index
-  uint32_t bytes;  // 4 * sx * sy * sz when < 2^32 (buffer-load path with 32-bit offsets), else 0
+  uint32_t sx, sy, sz;  // reference sizes
+  uint32_t ys, xs;      // linear: sz, sy*sz; bricked: samples per brick step along y, x
+  uint32_t bytes;       // buffer num_records: device bytes (<= 4 GiB, saturated), else 0
 };
+
+__host__ __device__ __forceinline__ uint32_t grid_bricks(uint32_t n) { return (n + kBrick - 1) / kBrick; }
+
+// grid kernel modes: bit 0 = buffer loads with 32-bit byte offsets (else 64-bit
+// addresses), bit 1 = bricked (else linear). Separate kernel instantiations,
+// so the rare 64-bit path does not set the common one's register budget.
+constexpr int kGridBuf = 1, kGridBricked = 2;
+
+// sample offsets of coordinate i along each axis (their sum addresses sample (x, y, z))
+template <int kMode>
+__device__ __forceinline__ uint32_t grid_ox(const GridDev &g, uint32_t i) {
+  if constexpr (kMode & kGridBricked) return (i >> 2) * g.xs + ((i & 3u) << 4);
+  return i * g.xs;
+}
+template <int kMode>
+__device__ __forceinline__ uint32_t grid_oy(const GridDev &g, uint32_t i) {
+  if constexpr (kMode & kGridBricked) return (i >> 2) * g.ys + ((i & 3u) << 2);
+  return i * g.ys;
+}
+template <int kMode>
+__device__ __forceinline__ uint32_t grid_oz(uint32_t i) {
+  if constexpr (kMode & kGridBricked) return ((i >> 2) << 6) + (i & 3u);
+  return i;
+}
 
 // gfx9 buffer resource word 3 (raw dword access, no swizzle)
 constexpr int kBufWord3 = 0x00020000;
 
-template <class CT>
+template <int kMode, class CT>
 __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell, CT &cnt) {
   cnt.add(C_GRID_SDF, 1);
   p = f3{(p.x + 1.0f) / 2.0f, (p.y + 1.0f) / 2.0f, (p.z + 1.0f) / 2.0f};
@@ -637,31 +676,27 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   if (i1x == i0x) { ax = 1.0f; bx = 0.0f; }
   if (i1y == i0y) { ay = 1.0f; by = 0.0f; }
   if (i1z == i0z) { az = 1.0f; bz = 0.0f; }
-  // the 8 taps (x*sy+y)*sz+z (grid_raytracing.hpp:13-15) as one base index plus
-  // per-axis steps of 0 (c1 == c0) or one sample
-  const uint32_t base = g.small ? __umul24(__umul24(i0x, g.sy) + i0y, g.sz) + i0z
-                                : (i0x * g.sy + i0y) * g.sz + i0z;
-  const uint32_t dz = i1z - i0z;
-  const uint32_t dy = i1y != i0y ? g.sz : 0u;
-  const uint32_t dx = i1x != i0x ? g.syz : 0u;
+  // the 8 taps sdf(c0/c1 per axis) in the reference's order (grid_raytracing.cpp:41-49)
+  const uint32_t x0 = grid_ox<kMode>(g, i0x), x1 = grid_ox<kMode>(g, i1x);
+  const uint32_t y0 = grid_oy<kMode>(g, i0y), y1 = grid_oy<kMode>(g, i1y);
+  const uint32_t z0 = grid_oz<kMode>(i0z), z1 = grid_oz<kMode>(i1z);
+  const uint32_t o00 = x0 + y0, o01 = x0 + y1, o10 = x1 + y0, o11 = x1 + y1;
   float p0, p1, p2, p3, p4, p5, p6, p7;
-  if (g.bytes) {  // buffer loads: 32-bit byte offsets, no 64-bit address arithmetic
+  if constexpr ((kMode & kGridBuf) != 0) {  // buffer loads: 32-bit byte offsets, no 64-bit address arithmetic
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.v), 0, (int)g.bytes, kBufWord3);
-    const uint32_t o0 = base << 2, z4 = dz << 2, y4 = dy << 2, o4 = o0 + (dx << 2);
-    p0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0, 0, 0));
-    p1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + z4, 0, 0));
-    p2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + y4, 0, 0));
-    p3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o0 + y4 + z4, 0, 0));
-    p4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4, 0, 0));
-    p5 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + z4, 0, 0));
-    p6 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + y4, 0, 0));
-    p7 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o4 + y4 + z4, 0, 0));
+    p0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z0) << 2, 0, 0));
+    p1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z1) << 2, 0, 0));
+    p2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z0) << 2, 0, 0));
+    p3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z1) << 2, 0, 0));
+    p4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z0) << 2, 0, 0));
+    p5 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z1) << 2, 0, 0));
+    p6 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z0) << 2, 0, 0));
+    p7 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z1) << 2, 0, 0));
   } else {
-    const float *__restrict__ v0 = g.v + base;
-    const float *__restrict__ v1 = v0 + dx;
-    p0 = v0[0]; p1 = v0[dz]; p2 = v0[dy]; p3 = v0[dy + dz];
-    p4 = v1[0]; p5 = v1[dz]; p6 = v1[dy]; p7 = v1[dy + dz];
+    const float *__restrict__ v = g.v;
+    p0 = v[(size_t)o00 + z0]; p1 = v[(size_t)o00 + z1]; p2 = v[(size_t)o01 + z0]; p3 = v[(size_t)o01 + z1];
+    p4 = v[(size_t)o10 + z0]; p5 = v[(size_t)o10 + z1]; p6 = v[(size_t)o11 + z0]; p7 = v[(size_t)o11 + z1];
   }
   float res = 0.0f;
   res += p0 * bx * by * bz;
@@ -672,11 +707,11 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   res += p5 * ax * by * az;
   res += p6 * ax * ay * bz;
   res += p7 * ax * ay * az;
-  if (cell) *cell = base;
+  if (cell) *cell = (i0x * g.sy + i0y) * g.sz + i0z;  // hit primitive: the c0 sample's reference index
   return res;
 }
 
-template <class CT>
+template <int kMode, class CT>
 __device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  // grid_raytracing.cpp:64-89
   const float E = 1e-3f;
   const float xl = (p.x - E >= -1.0f) ? p.x - E : p.x, xr = (p.x + E <= 1.0f) ? p.x + E : p.x;
@@ -689,7 +724,7 @@ __device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  //
   for (int k = 0; k < 3; ++k) {
     const f3 pr{k == 0 ? xr : p.x, k == 1 ? yr : p.y, k == 2 ? zr : p.z};
     const f3 pl{k == 0 ? xl : p.x, k == 1 ? yl : p.y, k == 2 ? zl : p.z};
-    const float dk = grid_sdf(g, pr, nullptr, cnt) - grid_sdf(g, pl, nullptr, cnt);
+    const float dk = grid_sdf<kMode>(g, pr, nullptr, cnt) - grid_sdf<kMode>(g, pl, nullptr, cnt);
     dx = k == 0 ? dk : dx;
     dy = k == 1 ? dk : dy;
     dz = k == 2 ? dk : dz;
@@ -698,7 +733,7 @@ __device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  //
 }
 
 // grid_raytracing.cpp:93-125. Returns hit and leaves the hit point in *hp.
-template <class CT>
+template <int kMode, class CT>
 __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
                                            float &out_t, f3 &hp, uint32_t &cell, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -710,7 +745,7 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   p = vstd_max(p, f3{-1.0f, -1.0f, -1.0f});
   p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
   while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
-    const float s = grid_sdf(g, p, &cell, cnt);
+    const float s = grid_sdf<kMode>(g, p, &cell, cnt);
     if (s < 1e-3f) {
       out_t = t + s;
       hp = p;
@@ -722,28 +757,28 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   return false;
 }
 
-template <class CT>
+template <int kMode, class CT>
 __device__ __forceinline__ Hit grid_intersect(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
                                               CT &cnt) {
   Hit h = miss_hit();
   f3 p;
   uint32_t cell;
-  if (grid_march(g, o, d, tNear, tFar, h.t, p, cell, cnt)) {
+  if (grid_march<kMode>(g, o, d, tNear, tFar, h.t, p, cell, cnt)) {
     h.hit = true;
-    h.n = grid_normal(g, p, cnt);
+    h.n = grid_normal<kMode>(g, p, cnt);
     h.prim = (int64_t)cell;
   } else {
     h.t = kInf;
   }
   return h;
 }
-template <class CT>
+template <int kMode, class CT>
 __device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
                                               CT &cnt) {
   float t;
   f3 p;
   uint32_t cell;
-  return grid_march(g, o, d, tNear, tFar, t, p, cell, cnt);
+  return grid_march<kMode>(g, o, d, tNear, tFar, t, p, cell, cnt);
 }
 
 // ----------------------------------------------------------------- octree --
