@@ -369,9 +369,11 @@ def main():
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     use_dist = world > 1 or a.dist
-    pmc = None
+    pmc, pmc_extra = None, {}
     if not use_dist and not a.no_pmc:
         pmc = pmc_traffic(a.workload, W_IMG, H_IMG, a.group)  # child processes, before this one inits the GPU
+        if not a.no_extra:  # the SDF-grid sphere march (north star: >= 60 % of HBM peak)
+            pmc_extra["grid"] = pmc_traffic("grid", W_IMG, H_IMG, a.group)
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
@@ -446,6 +448,9 @@ def main():
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_extra:
         out["extra"] = run_extras(min(a.warmup, 16), min(a.steps, 64), a.streams, a.group)
+        for key, (tb, detail) in pmc_extra.items():
+            out["extra"][key]["roofline"]["traffic"] = None if tb is None else round(tb)
+            out["extra"][key]["roofline"]["traffic_detail"] = detail
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:

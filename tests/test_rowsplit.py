@@ -91,6 +91,44 @@ def test_batched_frames_equal_single_frames(gpu, name, W, H, mode, tiled):
         assert torch.equal(t.view(torch.int32), bufs[k][1].view(torch.int32)), f"frame {k}"
 
 
+@pytest.mark.parametrize("name,W,H", [("stanford-bunny.obj", 200, 120), ("example_grid.grid", 9, 7),
+                                      ("sdf_6.octree", 130, 77)])
+def test_batched_launches_repeat_across_streams(gpu, name, W, H):
+    """The batch path's per-stream work queues: launches back to back on two
+    streams (each launch's last wave resets its stream's queue for the next)
+    give the same frames as one rt_render_device per frame; 9x7 has fewer
+    8x8 tiles than the grid has waves."""
+    from rtamd import _lib
+    from rtamd import workloads as WL
+    sc = S.gpu_scene(name)
+    sc.set_plane(None)
+    orbit = WL.orbit_positions(64)
+    prm = [WL.params_for(orbit[(5 * k) % 64], W, H, gpu.ShadingMode.Normal) for k in range(8)]
+    ref = []
+    for p in prm:
+        c = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+        sc.render_device(p, c.data_ptr(), t.data_ptr(), W, H, clear=True)
+        ref.append((c, t))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for rep in range(6):
+        st = streams[rep % 2]
+        n = 8 if rep % 3 else 5
+        bufs = [(torch.full((H, W), 7, dtype=torch.int32, device="cuda"),
+                 torch.zeros((H, W), dtype=torch.float32, device="cuda")) for _ in range(n)]
+        torch.cuda.synchronize()
+        sc.render_device_frames(prm[:n], [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs], W, H,
+                                _lib.RT_FLAG_CLEAR, stream=st.cuda_stream)
+        outs.append(bufs)
+    torch.cuda.synchronize()
+    for rep, bufs in enumerate(outs):
+        for k, (c, t) in enumerate(bufs):
+            assert torch.equal(c, ref[k][0]), f"launch {rep} frame {k}"
+            assert torch.equal(t.view(torch.int32), ref[k][1].view(torch.int32)), f"launch {rep} frame {k}"
+
+
 def test_hits_only_needs_clear(gpu):
     from rtamd import _lib
     sc = S.gpu_scene("cube.obj")

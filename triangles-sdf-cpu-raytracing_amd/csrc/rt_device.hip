@@ -9,8 +9,12 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rtamd.h"
@@ -63,6 +67,7 @@ struct MeshS {
   static constexpr int kFields = 3;
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   static constexpr int kMinWaves = 1;
+  static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
   MeshDev d;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
@@ -94,6 +99,7 @@ struct GridS {
   static constexpr int kFields = 1;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_GRID_WAVES;
+  static constexpr int kQueueGroup = 4;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -110,6 +116,7 @@ struct OctS {
   static constexpr int kFields = 2;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
+  static constexpr int kQueueGroup = 2;
   OctDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -287,22 +294,10 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 // centre-out order that dispatches the model tiles first (octree 4K primary
 // 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
 
-template <class S, int SLOTS, bool GENERAL, int DIAG>
-__device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
-                                            unsigned long long *counters, uint32_t *stk) {
-  typename CntSel<DIAG>::T cnt{};
-  unsigned long long t_start = 0;
-  if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t bx = blockIdx.x, by = blockIdx.y;
-  if (DIAG == 0 && fa.order) {  // cost-ordered schedule: this block renders tile order[b]
-    const uint32_t tl = fa.order[blockIdx.y * gridDim.x + blockIdx.x];
-    bx = tl % gridDim.x;
-    by = tl / gridDim.x;
-  }
-  const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
-  const int xo = bx * kTile + (wave & 1) * 8 + (lane & 7);
-  const int yl = by * kTile + (wave >> 1) * 8 + (lane >> 3);
+// One pixel per lane of the wave's 8x8 tile: column xo, rank-local row yl.
+template <class S, int SLOTS, bool GENERAL, int DIAG, class CT>
+__device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
+                                              CT &cnt, uint32_t *stk, int xo, int yl) {
   const bool active = xo < fa.W && yl < fa.rows_local;
   // wave-cooperative primary path: every lane of the wave takes part
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
@@ -352,6 +347,24 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
       fb_store(fa.t + idx, t, peer);
     }
   }
+}
+
+template <class S, int SLOTS, bool GENERAL, int DIAG>
+__device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
+                                            unsigned long long *counters, uint32_t *stk) {
+  typename CntSel<DIAG>::T cnt{};
+  unsigned long long t_start = 0;
+  if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t bx = blockIdx.x, by = blockIdx.y;
+  if (DIAG == 0 && fa.order) {  // cost-ordered schedule: this block renders tile order[b]
+    const uint32_t tl = fa.order[blockIdx.y * gridDim.x + blockIdx.x];
+    bx = tl % gridDim.x;
+    by = tl / gridDim.x;
+  }
+  const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
+  render_pixels<S, SLOTS, GENERAL, DIAG>(sc, pl, fa, cnt, stk, bx * kTile + (wave & 1) * 8 + (lane & 7),
+                                         by * kTile + (wave >> 1) * 8 + (lane >> 3));
   if constexpr (DIAG == 0) {
     if (fa.cost) {  // this wave's duration; the tile keeps its slowest wave's
       const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
@@ -430,6 +443,74 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_wave
 void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   render_body<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[blockIdx.z], nullptr, stk);
+}
+
+// Persistent form of render_batch_kernel: a grid of just the resident blocks;
+// every wave pulls 8x8 pixel tiles (items) from a work queue until the batch
+// is drained, so a wave whose tile finishes early takes the next one at once
+// instead of waiting for the in-order workgroup dispatcher (which stalls
+// behind a full SE while other SEs have free slots). The queue is sharded per
+// XCD: item i belongs to head i % 8 (HW_REG_XCC_ID picks a wave's own head),
+// a wave whose head is drained moves on to the other seven, so the batch
+// completes whatever XCDs the grid lands on. The next item is claimed before
+// the current one is traced (its atomic's latency hides under the traversal).
+// The last wave out resets the heads for the next launch on the stream.
+struct PersistQ {
+  uint32_t *heads;   // 8 heads kHeadStride words apart; heads[8 * kHeadStride] = waves done
+  uint32_t items;    // frames * per_frame
+  uint32_t tiles_x, per_frame;  // items (groups of gx x gy wave tiles) per row / per frame
+  uint32_t waves;    // waves in the grid
+  uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
+  uint32_t stride;   // words between heads
+};
+// 4 KiB + 256 B apart: every head on its own memory channel's lines, so the
+// memory-side atomics of different heads do not queue behind each other
+// (RTAMD_QSTRIDE=<words> overrides it for A/B runs, at most kHeadStrideMax)
+constexpr int kHeadStride = 1088;
+constexpr int kHeadStrideMax = 4096;
+
+__device__ __forceinline__ uint32_t q_claim(uint32_t *head) {
+  uint32_t k = 0;
+  if ((threadIdx.x & 63) == 0) k = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(k);
+}
+
+template <class S, int SLOTS, bool GENERAL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
+void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
+  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  const int lane = threadIdx.x & 63;
+  uint32_t h = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
+  uint32_t hops = 0;
+  uint32_t k = q_claim(q.heads + h * q.stride);
+  NoCnt cnt{};
+  for (;;) {
+    uint32_t item = k * 8 + h;
+    while (item >= q.items) {  // head h drained: the next head, until all eight are
+      if (++hops == 8) break;
+      h = (h + 1) & 7;
+      k = q_claim(q.heads + h * q.stride);
+      item = k * 8 + h;
+    }
+    if (hops == 8) break;
+    const uint32_t knext = q_claim(q.heads + h * q.stride);
+    const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
+    const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
+    for (uint32_t j = 0; j < q.gy; ++j)
+      for (uint32_t i = 0; i < q.gx; ++i)
+        render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[f], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
+                                            (int)((ty * q.gy + j) * 8) + (lane >> 3));
+    k = knext;
+  }
+  if (lane == 0) {
+    uint32_t *done = q.heads + 8 * q.stride;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
+      // every wave has left its claim loop: no claim is in flight any more
+      for (int i = 0; i < 8; ++i)
+        __hip_atomic_store(q.heads + i * q.stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <class S, int SLOTS>
@@ -777,14 +858,98 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
   return RT_OK;
 }
 
+// Work-queue heads of render_persist_kernel, one set per (device, stream):
+// launches on one stream run in order, and each launch's last wave resets its
+// heads, so consecutive launches on a stream reuse them; concurrent streams
+// never share a set.
+std::mutex g_queue_mu;
+std::map<std::pair<int, hipStream_t>, uint32_t *> g_queues;
+
+uint32_t *stream_queue(hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_queue_mu);
+  auto it = g_queues.find({dev, stream});
+  if (it != g_queues.end()) return it->second;
+  void *p = nullptr;
+  if (hipMalloc(&p, (8 * kHeadStrideMax + 16) * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, (8 * kHeadStrideMax + 16) * sizeof(uint32_t)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  g_queues[{dev, stream}] = (uint32_t *)p;
+  return (uint32_t *)p;
+}
+
+// RTAMD_PERSIST=0 selects the one-block-per-16x16-tile dispatch (A/B switch).
+bool persist_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// wave tiles per queue item; RTAMD_PERSIST_G=1|2|4 overrides the scene's default (A/B switch)
+int persist_group(int dflt) {
+  static const int g = [] {
+    const char *e = std::getenv("RTAMD_PERSIST_G");
+    return e ? std::atoi(e) : 0;
+  }();
+  return (g == 1 || g == 2 || g == 4) ? g : dflt;
+}
+
+template <class S, int MAXD, bool GENERAL>
+int launch_persist_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, int group,
+                     hipStream_t stream) {
+  static int blocks = 0;
+  static int dev_cached = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (blocks == 0 || dev != dev_cached) {
+    int per_cu = 0, cus = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_persist_kernel<S, MAXD, GENERAL>,
+                                                         kBlock, 0));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    blocks = std::max(1, per_cu) * std::max(1, cus);
+    dev_cached = dev;
+  }
+  uint32_t *heads = stream_queue(stream);
+  if (!heads) return set_err(RT_E_DEVICE, "work-queue allocation failed");
+  PersistQ q;
+  q.heads = heads;
+  static const uint32_t stride = [] {
+    const char *e = std::getenv("RTAMD_QSTRIDE");
+    const int v = e ? std::atoi(e) : 0;
+    return (uint32_t)((v >= 1 && v <= kHeadStrideMax) ? v : kHeadStride);
+  }();
+  q.stride = stride;
+  q.gx = group >= 2 ? 2 : 1;
+  q.gy = group >= 4 ? 2 : 1;
+  q.tiles_x = (uint32_t)((fb.f[0].W + 8 * q.gx - 1) / (8 * q.gx));
+  q.per_frame = q.tiles_x * (uint32_t)((fb.f[0].rows_local + 8 * q.gy - 1) / (8 * q.gy));
+  q.items = q.per_frame * (uint32_t)n;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
+  q.waves = grid * (kBlock / 64);
+  render_persist_kernel<S, MAXD, GENERAL><<<grid, kBlock, 0, stream>>>(sc, pl, fb, q);
+  return RT_OK;
+}
+
 template <class S, int MAXD>
-void launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
-                    hipStream_t stream) {
+int launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
+                   hipStream_t stream) {
+  if (persist_enabled()) {
+    const int group = persist_group(S::kQueueGroup);
+    return general ? launch_persist_t<S, MAXD, true>(sc, pl, fb, n, group, stream)
+                   : launch_persist_t<S, MAXD, false>(sc, pl, fb, n, group, stream);
+  }
   const dim3 grid((fb.f[0].W + kTile - 1) / kTile, (fb.f[0].rows_local + kTile - 1) / kTile, n);
   if (general)
     render_batch_kernel<S, MAXD, true><<<grid, kBlock, 0, stream>>>(sc, pl, fb);
   else
     render_batch_kernel<S, MAXD, false><<<grid, kBlock, 0, stream>>>(sc, pl, fb);
+  return RT_OK;
 }
 
 // One launch for n <= kMaxBatch frames of equal size / tile (blockIdx order).
@@ -796,34 +961,36 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
     fb.f[i].order = nullptr;
     fb.f[i].cost = nullptr;
   }
+  int rc = RT_OK;
   if (s->kind == RT_SCENE_MESH) {
     MeshS sc{mesh_dev(s)};
     switch (s->maxd) {
-      case 4: launch_batch_t<MeshS, 4>(sc, s->plane, fb, n, general, stream); break;
-      case 7: launch_batch_t<MeshS, 7>(sc, s->plane, fb, n, general, stream); break;
-      case 15: launch_batch_t<MeshS, 15>(sc, s->plane, fb, n, general, stream); break;
-      default: launch_batch_t<MeshS, 31>(sc, s->plane, fb, n, general, stream); break;
+      case 4: rc = launch_batch_t<MeshS, 4>(sc, s->plane, fb, n, general, stream); break;
+      case 7: rc = launch_batch_t<MeshS, 7>(sc, s->plane, fb, n, general, stream); break;
+      case 15: rc = launch_batch_t<MeshS, 15>(sc, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<MeshS, 31>(sc, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
     const GridDev gd = grid_dev(s);
     switch (grid_mode(s, gd)) {
       case kGridBuf | kGridBricked:
-        launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream);
+        rc = launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream);
         break;
-      case kGridBricked: launch_batch_t<GridS<kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream); break;
-      default: launch_batch_t<GridS<kGridBuf>, 1>({gd}, s->plane, fb, n, general, stream); break;
+      case kGridBricked: rc = launch_batch_t<GridS<kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<GridS<kGridBuf>, 1>({gd}, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
-      case 4: launch_batch_t<OctS, 4>(sc, s->plane, fb, n, general, stream); break;
-      case 7: launch_batch_t<OctS, 7>(sc, s->plane, fb, n, general, stream); break;
-      case 15: launch_batch_t<OctS, 15>(sc, s->plane, fb, n, general, stream); break;
-      default: launch_batch_t<OctS, 31>(sc, s->plane, fb, n, general, stream); break;
+      case 4: rc = launch_batch_t<OctS, 4>(sc, s->plane, fb, n, general, stream); break;
+      case 7: rc = launch_batch_t<OctS, 7>(sc, s->plane, fb, n, general, stream); break;
+      case 15: rc = launch_batch_t<OctS, 15>(sc, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<OctS, 31>(sc, s->plane, fb, n, general, stream); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
   }
+  if (rc) return rc;
   HIP_TRY(hipGetLastError());
   return RT_OK;
 }
