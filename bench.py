@@ -244,7 +244,9 @@ def pmc_traffic(workload, W, H, group, frames=32):
         return None, {"error": "rocprofv3 not found"}
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}
-    kname = "render_batch_kernel" if group > 1 else "render_kernel"
+    # the batch path's kernel: render_persist_kernel (work queue) or, with
+    # RTAMD_PERSIST=0, render_batch_kernel; one frame per launch: render_kernel
+    knames = ("render_persist_kernel", "render_batch_kernel") if group > 1 else ("render_kernel",)
     tmp = tempfile.mkdtemp(prefix="rtamd_pmc_", dir="/tmp")
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -260,10 +262,10 @@ def pmc_traffic(workload, W, H, group, frames=32):
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if kname in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                        if any(k in row["Kernel_Name"] for k in knames) and row["Counter_Name"] == ctr:
                             per.append(float(row["Counter_Value"]))
             if not per:
-                return None, {"error": f"no {ctr} rows for {kname}"}
+                return None, {"error": f"no {ctr} rows for {knames}"}
             vals[ctr] = sum(per) / len(per)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

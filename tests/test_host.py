@@ -98,10 +98,13 @@ def test_bvh8_identical_to_reference_builder(rt, ref, name):
 
 @pytest.mark.parametrize("seed,ntri,mode", [(1, 1, "rand"), (2, 7, "rand"), (3, 9, "rand"), (4, 300, "rand"),
                                             (5, 2000, "rand"), (6, 64, "same"), (7, 500, "grid"),
-                                            (8, 100, "flat")])
+                                            (8, 100, "flat"), (9, 30000, "grid"), (10, 12000, "same"),
+                                            (11, 40000, "rand")])
 def test_bvh8_edge_cases(rt, ref, seed, ntri, mode):
     """Tiny meshes (root leaf), duplicate triangles (all SAH keys tie), axis-aligned
-    grids of triangles (many equal keys) and flat meshes (zero-area boxes)."""
+    grids of triangles (many equal keys) and flat meshes (zero-area boxes). The
+    large cases run the parallel sort (ranges >= 4096 ids) and the concurrent
+    axes, whose tie order must equal the serial std::sort's."""
     rng = np.random.default_rng(seed)
     if mode == "same":
         v = np.tile(rng.normal(size=(3, 3)), (ntri, 1))

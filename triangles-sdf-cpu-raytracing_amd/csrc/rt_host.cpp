@@ -221,24 +221,114 @@ struct HNode {
   Box box[8];
 };
 
+// std::sort, in parallel, with the exact permutation libstdc++'s serial
+// std::sort produces (introsort: median-of-three pivot moved to the front,
+// unguarded Hoare partition, recursion on the right part and a loop on the
+// left, heapsort below depth 2*lg(n), ranges of <= 16 left for a final
+// insertion sort). The two parts of a partition are independent, so the right
+// part becomes an OpenMP task. The final insertion sort is stable and never
+// moves an element across a partition boundary (left part <= pivot <= right
+// part), so insertion-sorting each <= 16 leaf range where the loop leaves it
+// gives the same sequence as the one final pass over the whole range.
+// Equal keys therefore end in the same order as the serial sort, which the
+// SAH sweeps (and so the tree) depend on. Keys: K[id], compared with <.
+namespace psort {
+constexpr ptrdiff_t kThreshold = 16;    // libstdc++ _S_threshold
+constexpr ptrdiff_t kTaskMin = 4096;    // right parts at least this long become tasks
+
+struct Less {
+  const float *K;
+  bool operator()(uint32_t a, uint32_t b) const { return K[a] < K[b]; }
+};
+
+inline void insertion(uint32_t *first, uint32_t *last, Less c) {  // std::__insertion_sort
+  if (first == last) return;
+  for (uint32_t *i = first + 1; i != last; ++i) {
+    const uint32_t v = *i;
+    if (c(v, *first)) {
+      std::move_backward(first, i, i + 1);
+      *first = v;
+    } else {  // std::__unguarded_linear_insert
+      uint32_t *l = i, *n = i - 1;
+      while (c(v, *n)) { *l = *n; l = n; --n; }
+      *l = v;
+    }
+  }
+}
+
+inline void median_to_first(uint32_t *r, uint32_t *a, uint32_t *b, uint32_t *cc, Less c) {
+  if (c(*a, *b)) {
+    if (c(*b, *cc)) std::iter_swap(r, b);
+    else if (c(*a, *cc)) std::iter_swap(r, cc);
+    else std::iter_swap(r, a);
+  } else if (c(*a, *cc)) std::iter_swap(r, a);
+  else if (c(*b, *cc)) std::iter_swap(r, cc);
+  else std::iter_swap(r, b);
+}
+
+inline uint32_t *partition(uint32_t *first, uint32_t *last, uint32_t *pivot, Less c) {
+  for (;;) {
+    while (c(*first, *pivot)) ++first;
+    --last;
+    while (c(*pivot, *last)) --last;
+    if (!(first < last)) return first;
+    std::iter_swap(first, last);
+    ++first;
+  }
+}
+
+void loop(uint32_t *first, uint32_t *last, ptrdiff_t depth, Less c) {  // std::__introsort_loop
+  while (last - first > kThreshold) {
+    if (depth == 0) {  // std::__partial_sort(first, last, last): heapsort, output sorted
+      std::make_heap(first, last, c);
+      std::sort_heap(first, last, c);
+      return;
+    }
+    --depth;
+    uint32_t *mid = first + (last - first) / 2;
+    median_to_first(first, first + 1, mid, last - 1, c);
+    uint32_t *cut = partition(first + 1, last, first, c);
+    if (last - cut >= kTaskMin) {
+#pragma omp task firstprivate(cut, last, depth, c)
+      loop(cut, last, depth, c);
+    } else {
+      loop(cut, last, depth, c);
+    }
+    last = cut;
+  }
+  insertion(first, last, c);
+}
+
+inline ptrdiff_t lg(ptrdiff_t n) { return (ptrdiff_t)(sizeof(long long) * 8 - 1 - __builtin_clzll((unsigned long long)n)); }
+
+void sort(uint32_t *first, uint32_t *last, const float *K) {
+  if (last - first < 2) return;
+  Less c{K};
+  if (last - first < kTaskMin) {
+    std::sort(first, last, c);
+    return;
+  }
+#pragma omp taskgroup
+  loop(first, last, 2 * lg(last - first), c);
+}
+}  // namespace psort
+
 struct Builder {
   std::vector<uint32_t> cur, scrY, scrZ;  // triangle ids, 'cur' = mesh.indices order
-  std::vector<Box> triBox, leftB, rightB;
+  std::vector<Box> triBox, rightB[3];
   std::vector<float> key[3];
   std::vector<HNode> nodes;
 
   struct Div { bool divided = false; size_t divider = (size_t)-1; float sah = kInf; };
 
-  // triangles_raytracing.cpp:30-117 in index units [start, end)
+  // triangles_raytracing.cpp:30-117 in index units [start, end). The suffix
+  // boxes are kept per axis (the three axes may run concurrently); the prefix
+  // box is accumulated in the SAH sweep itself. Box unions are min/max, exact
+  // in any order, so every box equals the reference's m_leftBoxes /
+  // m_rightBoxes entry, and the parent box is the full suffix box.
   Div try_axis(std::vector<uint32_t> &ids, size_t start, size_t end, int axis) {
-    const float *K = key[axis].data();
-    std::sort(ids.begin() + start / 3, ids.begin() + end / 3,
-              [K](uint32_t a, uint32_t b) { return K[a] < K[b]; });
-    for (size_t b = start / 3; b != end / 3; ++b) {
-      Box &box = leftB[b];
-      box = (b == start / 3) ? empty_box() : leftB[b - 1];
-      grow(box, triBox[ids[b]]);
-    }
+    psort::sort(ids.data() + start / 3, ids.data() + end / 3, key[axis].data());
+    std::vector<Box> &rightB = rightB_for(axis);
     for (size_t r = start / 3; r != end / 3; ++r) {
       size_t b = end / 3 - r + start / 3 - 1;
       Box &box = rightB[b];
@@ -247,11 +337,13 @@ struct Builder {
     }
     Div res;
     res.sah = static_cast<float>(end - start) / 3.0f;
-    const float parentSA = surface_area(leftB[end / 3 - 1]);
+    const float parentSA = surface_area(rightB[start / 3]);
+    Box left = empty_box();
     for (size_t d = start + 3; d < end; d += 3) {
+      grow(left, triBox[ids[d / 3 - 1]]);
       const float lc = static_cast<float>(d - start) / 3.0f;
       const float rc = static_cast<float>(end - start) / 3.0f - lc;
-      const float c = 0.2f + surface_area(leftB[d / 3 - 1]) / parentSA * lc +
+      const float c = 0.2f + surface_area(left) / parentSA * lc +
                       surface_area(rightB[d / 3]) / parentSA * rc;
       if (c < res.sah) { res.sah = c; res.divider = d; res.divided = true; }
     }
@@ -264,6 +356,9 @@ struct Builder {
     }
     return res;
   }
+  std::vector<Box> &rightB_for(int axis) { return rightB[axis]; }
+
+  static constexpr size_t kAxesTaskMin = 1024;  // triangles
 
   // triangles_raytracing.cpp:119-153
   Div try_divide(size_t start, size_t end) {
@@ -271,9 +366,19 @@ struct Builder {
     std::copy(cur.begin() + start / 3, cur.begin() + end / 3, scrY.begin() + start / 3);
     std::copy(cur.begin() + start / 3, cur.begin() + end / 3, scrZ.begin() + start / 3);
     const float curSAH = static_cast<float>(end - start) / 3.0f;
-    Div dx = try_axis(cur, start, end, 0);
-    Div dy = try_axis(scrY, start, end, 1);
-    Div dz = try_axis(scrZ, start, end, 2);
+    Div dx, dy, dz;
+    if (end - start >= 3 * kAxesTaskMin) {  // the three axes concurrently (disjoint scratch)
+#pragma omp task shared(dy)
+      dy = try_axis(scrY, start, end, 1);
+#pragma omp task shared(dz)
+      dz = try_axis(scrZ, start, end, 2);
+      dx = try_axis(cur, start, end, 0);
+#pragma omp taskwait
+    } else {
+      dx = try_axis(cur, start, end, 0);
+      dy = try_axis(scrY, start, end, 1);
+      dz = try_axis(scrZ, start, end, 2);
+    }
     const float m = std::min({curSAH, dx.sah, dy.sah, dz.sah});
     if (dx.sah == m) return dx;
     if (dy.sah == m) {
@@ -393,8 +498,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
   for (size_t t = 0; t < ntri; ++t) B.cur[t] = (uint32_t)t;
   B.scrY.resize(ntri);
   B.scrZ.resize(ntri);
-  B.leftB.resize(ntri);
-  B.rightB.resize(ntri);
+  for (int a = 0; a < 3; ++a) B.rightB[a].resize(ntri);
   B.nodes.reserve(ntri + 16);
   B.nodes.emplace_back();
 #pragma omp parallel
