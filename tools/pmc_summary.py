@@ -6,10 +6,10 @@ import sys
 from collections import defaultdict
 
 
-def summarise(root, kernel_substr="render_kernel"):
+def summarise(root, kernel_substr=os.environ.get("PMC_KERNEL", "render_kernel")):
     vals = defaultdict(list)
     durs = []
-    for f in sorted(glob.glob(os.path.join(root, "*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if kernel_substr not in row["Kernel_Name"]:
