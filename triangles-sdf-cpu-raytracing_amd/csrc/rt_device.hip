@@ -63,10 +63,13 @@ struct FrameArgs {
 #ifndef RT_OCT_WAVES
 #define RT_OCT_WAVES 6
 #endif
+#ifndef RT_MESH_WAVES
+#define RT_MESH_WAVES 4
+#endif
 struct MeshS {
   static constexpr int kFields = 3;
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
-  static constexpr int kMinWaves = 1;
+  static constexpr int kMinWaves = RT_MESH_WAVES;
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
   MeshDev d;
   template <int B>
