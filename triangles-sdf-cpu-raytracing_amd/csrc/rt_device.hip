@@ -102,7 +102,9 @@ struct GridS {
   static constexpr int kFields = 1;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_GRID_WAVES;
-  static constexpr int kQueueGroup = 4;
+  // block dispatch: a grid tile is too short for the queue's claims to pay
+  // (256^3, 8 frames x 2 streams: 0.0506 ms/frame vs 0.0541 at 4 tiles per claim)
+  static constexpr int kQueueGroup = 0;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -436,10 +438,15 @@ void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
 // silhouette, the per-frame tail) finish, so only the batch's last frame
 // leaves a tail. The per-frame arguments travel in the kernarg segment
 // (uniform blockIdx.z index: scalar loads).
-constexpr int kMaxBatch = 8;
+#ifndef RT_MAX_BATCH
+#define RT_MAX_BATCH 8
+#endif
+constexpr int kMaxBatch = RT_MAX_BATCH;
 struct FrameBatch {
   FrameArgs f[kMaxBatch];
 };
+// the whole batch travels in the kernarg segment next to the scene, plane and queue words
+static_assert(sizeof(FrameBatch) + 256 <= 4096, "FrameBatch exceeds the 4 KiB kernel-argument budget");
 
 template <class S, int SLOTS, bool GENERAL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
@@ -483,19 +490,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_wave
 void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   const int lane = threadIdx.x & 63;
-  uint32_t h = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
-  uint32_t hops = 0;
+  const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
+  uint32_t h = xcc;
   uint32_t k = q_claim(q.heads + h * q.stride);
   NoCnt cnt{};
   for (;;) {
-    uint32_t item = k * 8 + h;
-    while (item >= q.items) {  // head h drained: the next head, until all eight are
-      if (++hops == 8) break;
-      h = (h + 1) & 7;
+    const uint32_t item = k * 8 + h;
+    if (item >= q.items) {
+      // head h drained: read all eight heads at once (lanes 0-7, one round
+      // trip) and claim from a head that still has items, the first one after
+      // this XCD's own; none left: done. A claim that loses the race to the
+      // last item just comes back here.
+      uint32_t v = 0xFFFFFFFFu;
+      if (lane < 8) v = __hip_atomic_load(q.heads + lane * q.stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t m = __ballot(lane < 8 && v < (q.items + 7u - (uint32_t)lane) / 8u) & 0xFFull;
+      if (m == 0) break;
+      const uint32_t rot = (uint32_t)(((m >> (xcc + 1)) | (m << (7 - xcc))) & 0xFFull);  // bit i: head xcc+1+i
+      h = (xcc + 1 + (uint32_t)__builtin_ctz(rot)) & 7u;
       k = q_claim(q.heads + h * q.stride);
-      item = k * 8 + h;
+      continue;
     }
-    if (hops == 8) break;
     const uint32_t knext = q_claim(q.heads + h * q.stride);
     const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
@@ -894,7 +908,8 @@ bool persist_enabled() {
   return on;
 }
 
-// wave tiles per queue item; RTAMD_PERSIST_G=1|2|4 overrides the scene's default (A/B switch)
+// wave tiles per queue item (0: block dispatch); RTAMD_PERSIST_G=1|2|4 overrides
+// the scene's default (A/B switch)
 int persist_group(int dflt) {
   static const int g = [] {
     const char *e = std::getenv("RTAMD_PERSIST_G");
@@ -942,8 +957,13 @@ int launch_persist_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int 
 template <class S, int MAXD>
 int launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
                    hipStream_t stream) {
-  if (persist_enabled()) {
-    const int group = persist_group(S::kQueueGroup);
+  // Row-band tiles (a rank's share of a multi-GPU frame) take the block
+  // dispatch: with 1/N of the pixels per launch the queue's drain (a wave
+  // probes all 8 heads before it exits) and its launch-to-launch hand-over
+  // cost more than they balance (bunny 1080p, rank 0 of 4: 0.0415 vs 0.0336
+  // ms/frame; of 8: 0.037 vs 0.021; at N = 2 the two are level).
+  const int group = persist_group(S::kQueueGroup);
+  if (persist_enabled() && group > 0 && fb.f[0].nranks <= 1) {
     return general ? launch_persist_t<S, MAXD, true>(sc, pl, fb, n, group, stream)
                    : launch_persist_t<S, MAXD, false>(sc, pl, fb, n, group, stream);
   }
