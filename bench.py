@@ -225,6 +225,17 @@ def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None, fram
     return out
 
 
+def one_stream(scene, params, warmup, steps, W, H, group, rl):
+    """The same launches (group frames each) issued on ONE stream: launches do
+    not overlap, so the event-timed launch duration is the launch's own time
+    and bytes / duration is the kernel's rate without a second launch beside
+    it. Reported beside the default two-stream roofline."""
+    wall, kms, _ = run_single(scene, params, warmup, steps, W, H, inflight=1, batch=group)
+    achieved = rl["algorithmic_bytes_per_launch"] / (kms * 1e-3) / 1e9
+    return {"streams": 1, "ms_per_step": round(wall * 1e3 / steps, 4), "kernel_ms": round(kms, 5),
+            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4)}
+
+
 def pmc_traffic(workload, W, H, group, frames=32):
     """HBM bytes per launch of the headline render kernel (launches of `group`
     frames, the timed region's launch shape) from rocprofv3 PMC counters,
@@ -318,10 +329,12 @@ def run_extras(warmup, steps, streams, group):
         orbit = WL.orbit_positions(64)
         prm = [WL.params_for(orbit[k % 64], W, H, rtamd.ShadingMode.Normal) for k in range(warmup + steps)]
         wall, kms, _ = run_single(sc, prm, warmup, steps, W, H, inflight=streams, batch=group)
+        rl = roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps, group)
         out[key] = {"workload": f"{desc}, {W}x{H} primary rays, same orbit",
                     "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
-                    "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
-                    "roofline": roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps, group)}
+                    "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps, "roofline": rl}
+        if streams > 1:
+            out[key]["roofline_one_stream"] = one_stream(sc, prm, warmup, steps, W, H, group, rl)
         sc.close()
         torch.cuda.synchronize()
     return out
@@ -443,6 +456,8 @@ def main():
     }
     if latency is not None:
         out["frame_latency"] = latency
+    if not use_dist and a.streams > 1:
+        out["roofline_one_stream"] = one_stream(scene, params, a.warmup, a.steps, W_IMG, H_IMG, a.group, rl)
     if use_dist and rank == 0:
         out["frame_check"] = {"assembled_equals_single_render": check_equal,
                               "backend": dist.get_backend(), "exchange": rs.exchange,

@@ -84,9 +84,15 @@ __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uin
 
 // One leaf: its local best, first wins among equal t (strict `>` in triangle
 // order, triangles_raytracing.cpp:324-331). The leaf's triangles are read in
-// batches of 4 with all 12 loads in flight together (the triangle array is
-// padded by 8 entries, so reading past a short leaf is in bounds and the
-// extra lanes are discarded), instead of one memory round trip per triangle.
+// batches of RT_LEAF_BATCH with all their loads in flight together (the
+// triangle array is padded by 8 entries, so reading past a short leaf is in
+// bounds and the extra lanes are discarded), instead of one memory round trip
+// per triangle. Triangles per batch: 2 frees the VGPRs
+// the 4-wave mesh kernel needs (RT_MESH_WAVES, rt_device.hip); at the
+// compiler's 3 waves, 4 per batch is faster (bunny 0.1191 vs 0.1234 ms).
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 2
+#endif
 template <class CT>
 __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, uint32_t w, f3 o,
                                           f3 d, float &lt, uint32_t &lk, CT &cnt) {
@@ -95,19 +101,20 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
   cnt.add(C_BVH_LEAF, 1);
   cnt.add(C_BVH_TRI, n);
   const float4 *q = reinterpret_cast<const float4 *>(tris + first);
-  for (uint32_t base = 0; base < n; base += 4) {
-    float4 a[4], b[4], c[4];
+  constexpr uint32_t B = RT_LEAF_BATCH;
+  for (uint32_t base = 0; base < n; base += B) {
+    float4 a[B], b[B], c[B];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < B; ++k) {
       a[k] = q[3 * (base + k)];
       b[k] = q[3 * (base + k) + 1];
       c[k] = q[3 * (base + k) + 2];
     }
-    float tk[4];
+    float tk[B];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) tk[k] = tri_t(a[k], b[k], c[k], o, d);
+    for (uint32_t k = 0; k < B; ++k) tk[k] = tri_t(a[k], b[k], c[k], o, d);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (uint32_t k = 0; k < B; ++k)
       if (base + k < n && lt > tk[k]) { lt = tk[k]; lk = first + base + k; }
   }
 }
