@@ -123,6 +123,11 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
 // (a suffix of the sorted order) as a packed list of 3-bit ids + count. Also
 // returns the entry distance and child word of the first child to visit (the
 // child words arrive with the boxes: descending needs no extra load).
+// 1: expand_node skips sort8 in waves whose rays all enter <= 2 children with
+// distinct t (A/B switch; 0 always runs the network)
+#ifndef RT_EXPAND_FAST
+#define RT_EXPAND_FAST 1
+#endif
 template <bool FAST>
 __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node, f3 o, f3 inv,
                                             float tNear, float tFar, uint32_t &list,
@@ -145,18 +150,48 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
                       bx[6 * c + 5], o, inv, tNear, tFar);  // box: xMin xMax yMin yMax zMin zMax
     id[c] = (uint32_t)c;
   }
-  sort8(t, id);
-  list = 0;
-  cnt = 0;
-  tfirst = 0.0f;
   uint32_t first_id = 0;
+  bool sorted = false;
+  if constexpr (FAST && RT_EXPAND_FAST) {
+    // At most two children entered with distinct t: the network's output order
+    // of the entered children is plain ascending t (any correct sort gives
+    // it), so the wave skips sort8 when every lane is in that case. Ties (or
+    // three or more children) take the network: its order among equal keys
+    // is its own.
+    uint32_t m = 0;
 #pragma unroll
-  for (int i = 7; i >= 0; --i) {  // build from the back so the first visit ends in the low bits
-    if (!(t[i] < 0.0f)) {
-      list = (list << 3) | id[i];
-      cnt += 1;
-      tfirst = t[i];
-      first_id = id[i];
+    for (int c = 0; c < 8; ++c) m |= (t[c] < 0.0f) ? 0u : (1u << c);
+    const uint32_t pc = (uint32_t)__builtin_popcount(m);
+    const uint32_t ia = (uint32_t)__builtin_ctz(m | 0x100u), ib = 31u - (uint32_t)__builtin_clz(m | 1u);
+    float ta = t[0], tb = t[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) {
+      ta = (ia == (uint32_t)c) ? t[c] : ta;
+      tb = (ib == (uint32_t)c) ? t[c] : tb;
+    }
+    const bool slow = pc > 2 || (pc == 2 && !(ta != tb));
+    if (__ballot(slow) == 0) {
+      sorted = true;
+      const bool sw = pc == 2 && tb < ta;
+      first_id = sw ? ib : ia;
+      tfirst = pc == 0 ? 0.0f : (sw ? tb : ta);
+      cnt = pc;
+      list = pc == 0 ? 0u : pc == 1 ? ia : (sw ? (ib | (ia << 3)) : (ia | (ib << 3)));
+    }
+  }
+  if (!sorted) {
+    sort8(t, id);
+    list = 0;
+    cnt = 0;
+    tfirst = 0.0f;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {  // build from the back so the first visit ends in the low bits
+      if (!(t[i] < 0.0f)) {
+        list = (list << 3) | id[i];
+        cnt += 1;
+        tfirst = t[i];
+        first_id = id[i];
+      }
     }
   }
   uint32_t cf = cws[0];
