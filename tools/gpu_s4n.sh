@@ -5,6 +5,7 @@ O=$R/gpurun_out/s4n
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo TFAIL; tail -30 $O/tests.log; exit 1; }
 echo TESTS_OK
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke.log; exit 1; }
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { echo BFAIL; tail -20 $O/bench.err; exit 1; }
 echo BENCH_OK
 cd /tmp && export TMPDIR=/tmp && cd "$R"
