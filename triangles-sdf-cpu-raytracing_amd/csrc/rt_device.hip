@@ -713,7 +713,9 @@ GridDev grid_dev(const rt_scene *s) {
 }
 
 int grid_mode(const rt_scene *s, const GridDev &gd) {
-  return (gd.bytes ? kGridBuf : 0) | (s->grid_bricked ? kGridBricked : 0);
+  // buffer mode: 32-bit byte offsets and 24-bit stride multiplies (grid_mul)
+  const bool buf = gd.bytes != 0 && gd.xs < (1u << 24) && gd.ys < (1u << 24);
+  return (buf ? kGridBuf : 0) | (s->grid_bricked ? kGridBricked : 0);
 }
 
 // reference x-major values -> 4x4x4 bricks; one thread per bricked sample

@@ -668,6 +668,9 @@ __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, flo
 //    lines and neighbouring lanes and steps share them (256^3 grid, 1080p:
 //    0.0646 -> 0.0507 ms per frame). The padding up to a multiple of 4 per
 //    axis is never read (taps are at most size-1).
+#ifndef RT_GRID_MUL24
+#define RT_GRID_MUL24 1  // A/B switch: 0 keeps 32-bit multiplies in the tap addressing
+#endif
 constexpr uint32_t kBrick = 4;
 constexpr uint64_t kGridLinearMaxBytes = 4ull << 20;
 struct GridDev {
@@ -684,16 +687,26 @@ __host__ __device__ __forceinline__ uint32_t grid_bricks(uint32_t n) { return (n
 // so the rare 64-bit path does not set the common one's register budget.
 constexpr int kGridBuf = 1, kGridBricked = 2;
 
+// a * b for sample offsets. In buffer mode both factors are below 2^24
+// (grid_mode checks the strides) and the product below 2^30 (a sample
+// offset in a < 4 GiB buffer), so the full-rate 24-bit multiply is exact;
+// the 32-bit form compiles to the multi-pass v_mad_u64_u32, and the march is
+// VALU-bound (four of them per sdf evaluation).
+template <int kMode>
+__device__ __forceinline__ uint32_t grid_mul(uint32_t a, uint32_t b) {
+  if constexpr ((kMode & kGridBuf) != 0 && RT_GRID_MUL24) return __umul24(a, b);
+  return a * b;
+}
 // sample offsets of coordinate i along each axis (their sum addresses sample (x, y, z))
 template <int kMode>
 __device__ __forceinline__ uint32_t grid_ox(const GridDev &g, uint32_t i) {
-  if constexpr (kMode & kGridBricked) return (i >> 2) * g.xs + ((i & 3u) << 4);
-  return i * g.xs;
+  if constexpr (kMode & kGridBricked) return grid_mul<kMode>(i >> 2, g.xs) + ((i & 3u) << 4);
+  return grid_mul<kMode>(i, g.xs);
 }
 template <int kMode>
 __device__ __forceinline__ uint32_t grid_oy(const GridDev &g, uint32_t i) {
-  if constexpr (kMode & kGridBricked) return (i >> 2) * g.ys + ((i & 3u) << 2);
-  return i * g.ys;
+  if constexpr (kMode & kGridBricked) return grid_mul<kMode>(i >> 2, g.ys) + ((i & 3u) << 2);
+  return grid_mul<kMode>(i, g.ys);
 }
 template <int kMode>
 __device__ __forceinline__ uint32_t grid_oz(uint32_t i) {
