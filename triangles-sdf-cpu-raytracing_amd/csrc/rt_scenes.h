@@ -668,6 +668,9 @@ __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, flo
 //    lines and neighbouring lanes and steps share them (256^3 grid, 1080p:
 //    0.0646 -> 0.0507 ms per frame). The padding up to a multiple of 4 per
 //    axis is never read (taps are at most size-1).
+#ifndef RT_GRID_TAP_CACHE
+#define RT_GRID_TAP_CACHE 1  // A/B switch: 0 reloads the 8 taps at every march step
+#endif
 #ifndef RT_GRID_MUL24
 #define RT_GRID_MUL24 1  // A/B switch: 0 keeps 32-bit multiplies in the tap addressing
 #endif
@@ -717,8 +720,45 @@ __device__ __forceinline__ uint32_t grid_oz(uint32_t i) {
 // gfx9 buffer resource word 3 (raw dword access, no swizzle)
 constexpr int kBufWord3 = 0x00020000;
 
-template <int kMode, class CT>
-__device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell, CT &cnt) {
+// The 8 taps of one evaluation and the cell they belong to. The march keeps
+// the last cell's taps: a step that lands in the same cell (the same c0 and
+// c1 on every axis; near the surface steps are short) reuses them instead of
+// reloading 8 values, so it costs only the weights and the trilinear sum.
+// The values are the same samples, so the result is bitwise the same.
+struct GridTaps {
+  uint32_t i0x = 0xFFFFFFFFu, i0y = 0, i0z = 0, i1x = 0, i1y = 0, i1z = 0;
+  float v[8];
+};
+
+template <int kMode>
+__device__ __forceinline__ void grid_fetch(const GridDev &g, uint32_t i0x, uint32_t i0y, uint32_t i0z,
+                                           uint32_t i1x, uint32_t i1y, uint32_t i1z, float v[8]) {
+  // the 8 taps sdf(c0/c1 per axis) in the reference's order (grid_raytracing.cpp:41-49)
+  const uint32_t x0 = grid_ox<kMode>(g, i0x), x1 = grid_ox<kMode>(g, i1x);
+  const uint32_t y0 = grid_oy<kMode>(g, i0y), y1 = grid_oy<kMode>(g, i1y);
+  const uint32_t z0 = grid_oz<kMode>(i0z), z1 = grid_oz<kMode>(i1z);
+  const uint32_t o00 = x0 + y0, o01 = x0 + y1, o10 = x1 + y0, o11 = x1 + y1;
+  if constexpr ((kMode & kGridBuf) != 0) {  // buffer loads: 32-bit byte offsets, no 64-bit address arithmetic
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.v), 0, (int)g.bytes, kBufWord3);
+    v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z0) << 2, 0, 0));
+    v[1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z1) << 2, 0, 0));
+    v[2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z0) << 2, 0, 0));
+    v[3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z1) << 2, 0, 0));
+    v[4] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z0) << 2, 0, 0));
+    v[5] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z1) << 2, 0, 0));
+    v[6] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z0) << 2, 0, 0));
+    v[7] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z1) << 2, 0, 0));
+  } else {
+    const float *__restrict__ gv = g.v;
+    v[0] = gv[(size_t)o00 + z0]; v[1] = gv[(size_t)o00 + z1]; v[2] = gv[(size_t)o01 + z0]; v[3] = gv[(size_t)o01 + z1];
+    v[4] = gv[(size_t)o10 + z0]; v[5] = gv[(size_t)o10 + z1]; v[6] = gv[(size_t)o11 + z0]; v[7] = gv[(size_t)o11 + z1];
+  }
+}
+
+// SDFGrid::sdf(float3) (grid_raytracing.cpp:7-62). CACHE: taps from / into tc.
+template <int kMode, bool CACHE, class CT>
+__device__ __forceinline__ float grid_sdf_t(const GridDev &g, f3 p, uint32_t *cell, GridTaps &tc, CT &cnt) {
   cnt.add(C_GRID_SDF, 1);
   p = f3{(p.x + 1.0f) / 2.0f, (p.y + 1.0f) / 2.0f, (p.z + 1.0f) / 2.0f};
   p = p * f3{(float)(g.sx - 1), (float)(g.sy - 1), (float)(g.sz - 1)};
@@ -731,39 +771,34 @@ __device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell
   if (i1x == i0x) { ax = 1.0f; bx = 0.0f; }
   if (i1y == i0y) { ay = 1.0f; by = 0.0f; }
   if (i1z == i0z) { az = 1.0f; bz = 0.0f; }
-  // the 8 taps sdf(c0/c1 per axis) in the reference's order (grid_raytracing.cpp:41-49)
-  const uint32_t x0 = grid_ox<kMode>(g, i0x), x1 = grid_ox<kMode>(g, i1x);
-  const uint32_t y0 = grid_oy<kMode>(g, i0y), y1 = grid_oy<kMode>(g, i1y);
-  const uint32_t z0 = grid_oz<kMode>(i0z), z1 = grid_oz<kMode>(i1z);
-  const uint32_t o00 = x0 + y0, o01 = x0 + y1, o10 = x1 + y0, o11 = x1 + y1;
-  float p0, p1, p2, p3, p4, p5, p6, p7;
-  if constexpr ((kMode & kGridBuf) != 0) {  // buffer loads: 32-bit byte offsets, no 64-bit address arithmetic
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.v), 0, (int)g.bytes, kBufWord3);
-    p0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z0) << 2, 0, 0));
-    p1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o00 + z1) << 2, 0, 0));
-    p2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z0) << 2, 0, 0));
-    p3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o01 + z1) << 2, 0, 0));
-    p4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z0) << 2, 0, 0));
-    p5 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o10 + z1) << 2, 0, 0));
-    p6 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z0) << 2, 0, 0));
-    p7 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (o11 + z1) << 2, 0, 0));
+  float v[8];
+  if constexpr (CACHE) {
+    if (!(i0x == tc.i0x && i0y == tc.i0y && i0z == tc.i0z && i1x == tc.i1x && i1y == tc.i1y && i1z == tc.i1z)) {
+      grid_fetch<kMode>(g, i0x, i0y, i0z, i1x, i1y, i1z, tc.v);
+      tc.i0x = i0x; tc.i0y = i0y; tc.i0z = i0z; tc.i1x = i1x; tc.i1y = i1y; tc.i1z = i1z;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tc.v[k];
   } else {
-    const float *__restrict__ v = g.v;
-    p0 = v[(size_t)o00 + z0]; p1 = v[(size_t)o00 + z1]; p2 = v[(size_t)o01 + z0]; p3 = v[(size_t)o01 + z1];
-    p4 = v[(size_t)o10 + z0]; p5 = v[(size_t)o10 + z1]; p6 = v[(size_t)o11 + z0]; p7 = v[(size_t)o11 + z1];
+    grid_fetch<kMode>(g, i0x, i0y, i0z, i1x, i1y, i1z, v);
   }
   float res = 0.0f;
-  res += p0 * bx * by * bz;
-  res += p1 * bx * by * az;
-  res += p2 * bx * ay * bz;
-  res += p3 * bx * ay * az;
-  res += p4 * ax * by * bz;
-  res += p5 * ax * by * az;
-  res += p6 * ax * ay * bz;
-  res += p7 * ax * ay * az;
+  res += v[0] * bx * by * bz;
+  res += v[1] * bx * by * az;
+  res += v[2] * bx * ay * bz;
+  res += v[3] * bx * ay * az;
+  res += v[4] * ax * by * bz;
+  res += v[5] * ax * by * az;
+  res += v[6] * ax * ay * bz;
+  res += v[7] * ax * ay * az;
   if (cell) *cell = (i0x * g.sy + i0y) * g.sz + i0z;  // hit primitive: the c0 sample's reference index
   return res;
+}
+
+template <int kMode, class CT>
+__device__ __forceinline__ float grid_sdf(const GridDev &g, f3 p, uint32_t *cell, CT &cnt) {
+  GridTaps unused;
+  return grid_sdf_t<kMode, false>(g, p, cell, unused, cnt);
 }
 
 template <int kMode, class CT>
@@ -799,8 +834,9 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   f3 p = o + t * d;
   p = vstd_max(p, f3{-1.0f, -1.0f, -1.0f});
   p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
+  GridTaps tc;
   while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
-    const float s = grid_sdf<kMode>(g, p, &cell, cnt);
+    const float s = grid_sdf_t<kMode, RT_GRID_TAP_CACHE != 0>(g, p, &cell, tc, cnt);
     if (s < 1e-3f) {
       out_t = t + s;
       hp = p;
