@@ -5,43 +5,52 @@ Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355
 Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
 1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
 the pure intersection hot path), over a deterministic 64-frame camera orbit
-(SURVEY.md 8(d)). A "step" is one frame. The orbit's frames are independent:
---group (default 8) of them go out in ONE launch (blockIdx.z = frame), so a
-frame's last tiles (grazing rays at the silhouette, the per-frame tail) are
-covered by the next frames' tiles, and launches alternate over --streams
-(default 2) HIP streams with their own framebuffers, so one launch's tail
-overlaps the next launch. value = rays of all K frames / wall time of the K
-frames; the one-frame-at-a-time latency is reported beside it
-("frame_latency"). At N=1 the other BASELINE configs are measured the same way
-and reported under "extra" (rank 0): the SDF grid (configs[2]) on a 256^3 SDF
-of stanford-bunny generated on the GPU (stand-in: example_grid_large.grid is
-missing from the reference) and on the shipped 65^3 example_grid.grid; the
-octree (configs[3]) at 3840x2160 on a depth-8 generated octree (stand-in for
-example_octree_large.octree) and on the shipped sdf_6.octree; and the config-5
-mesh stand-in (stanford-bunny subdivided twice, 1,111,216 triangles) at
-3840x2160.
+(SURVEY.md 8(d)). A "step" is one frame. Orbit frames are independent: up to
+--group (8) of them go out in ONE launch (the persistent kernel pulls 8x8 pixel
+tiles of all of them from one work queue), and launches alternate over
+--streams (2) HIP streams with their own framebuffers. value = rays of all K
+frames / wall time of the K frames.
+
+Warm-up: every stream gets at least one full launch (and its work-queue state
+via rt_stream_prepare) before t0, whatever --warmup is, so nothing is
+allocated or first-used inside the timed region. The K timed frames are split
+into ceil(K / group) launches of near-equal size.
+
+At N=1 the other BASELINE configs are measured the same way under "extra"
+(rank 0): the SDF grid (configs[2]; 256^3 GPU-generated stand-in and the
+shipped 65^3), the octree (configs[3]; depth-8 stand-in and shipped sdf_6, both
+3840x2160), the config-5 mesh stand-in (1.1 M triangles, 3840x2160, one GPU)
+and the reference's DEFAULT shading mode on the bunny (plane + Lambert +
+shadows + reflections), reported as primary rays/s and as traced rays/s
+(primary + shadow + reflection rays, counted by the diagnostic kernel).
+
+Roofline (per workload): achieved = ALGORITHMIC bytes per launch (SURVEY 8(d)
+byte model on the reference's data layout, counted exactly by the diagnostic
+variant of the same kernel over the same frames) / the render kernel's launch
+duration (HIP events on the launch's own stream; frame-weighted, so a short
+last launch does not inflate it), against the 8 TB/s HBM peak. These bytes are
+served mostly by L1/L2 (every scene is cache-resident), so beside it:
+measured DRAM bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc
+passes, MI355X_MICROARCH.md's gfx950 correction), the VALU issue fraction
+(SQ_INSTS_VALU x 2 cycles per wave64 instruction on SIMD-32 / (1024 SIMDs x
+2.4 GHz x duration); the 4-cycle single-wave form beside it) and the L2 hit
+rate. "binding" names the largest of those fractions.
 
 Multi-GPU (torch.distributed.run, one process per GPU; rtamd.rowsplit): every
-frame is split into --band-rows (8) row bands dealt round-robin to the ranks
-(load balance: the model covers the middle rows), with the same launches
-(--group frames, --streams streams). Exchange p2p (default): each rank's
-kernel stores its HIT pixels straight into rank 0's frame slots over xGMI
-(IPC-mapped), and one 4-byte RCCL all-reduce per group signals completion;
-exchange gather: one RCCL gather per group of the packed bands (8 B/pixel) and
-a de-interleave on rank 0. Total work per step is fixed (one 1080p frame), so
-scaling is "strong"; value = pixels of all frames / max-over-ranks wall time.
-rank 0 checks that its last assembled frame equals a whole-frame render.
+frame is split into --band-rows (8) row bands dealt round-robin to the ranks,
+with the same launches. Exchange p2p (default): each rank's kernel stores its
+HIT pixels straight into rank 0's frame slots over xGMI (IPC-mapped) and one
+4-byte RCCL all-reduce per group signals completion; exchange gather: one RCCL
+gather per group of packed bands + a de-interleave on rank 0. Total work per
+step is one 1080p frame whatever N is ("strong"); value = pixels of all frames /
+max-over-ranks wall time. Every rank reports its own render-kernel time per
+launch (rank_kernel_ms; the max over ranks bounds the scaling). rank 0 checks
+that its last assembled frame equals a whole-frame render.
 
-Timing: W untimed warm-up frames, then exactly K frames between barrier +
-torch.cuda.synchronize() on both sides; max over ranks. Inputs are resident
-in HBM before the timed region. Roofline: algorithmic bytes per launch
-(SURVEY.md 8(d) byte model, counted exactly by a diagnostic variant of the
-same kernel over the same frames) / the render kernel's average launch
-duration (HIP events around each launch on its own stream; what rocprofv3's
-kernel stats report); the amortized rate (wall / K, launches overlap) is
-reported beside it. Peak 8.0 TB/s HBM.
-cpu_baseline: the oracle (C++ restatement of the reference's CPU path, with
-the ISPC kernels in scalar C++) on the host cores, rank 0 at N=1 only.
+cpu_baseline: the oracle (C++ restatement of the reference's CPU path, ISPC
+kernels as scalar C++) on every CPU this process is granted (the smallest of
+the affinity set, the cgroup quota and OMP_NUM_THREADS; see host_threads),
+OpenMP schedule(dynamic) over rows, rank 0 at N=1 only.
 """
 from __future__ import annotations
 
@@ -49,6 +58,7 @@ import argparse
 import ctypes
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -63,7 +73,23 @@ from rtamd import workloads as WL  # noqa: E402
 
 METRIC = "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+L2_PEAK_GBS = 34500.0  # aggregate L2 (MI355X_MICROARCH.md, L2 per XCD)
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock
 W_IMG, H_IMG = 1920, 1080
+
+# key -> (input, W, H, mode, description); the headline is "bunny"
+WORKLOADS = {
+    "bunny": ("stanford-bunny.obj", 1920, 1080, "primary", "shipped stanford-bunny.obj (69,451 triangles)"),
+    "grid": ("grid", 1920, 1080, "primary", WL.STANDINS["grid"]),
+    "grid_shipped": ("example_grid.grid", 1920, 1080, "primary", "shipped example_grid.grid (65^3)"),
+    "octree": ("octree", 3840, 2160, "primary", WL.STANDINS["octree"]),
+    "octree_shipped": ("sdf_6.octree", 3840, 2160, "primary", "shipped sdf_6.octree (depth 6)"),
+    "mesh_large": ("mesh_large", 3840, 2160, "primary", WL.STANDINS["mesh_large"] + ", 1 GPU"),
+    "default_mode": ("stanford-bunny.obj", 1920, 1080, "default",
+                     "stanford-bunny.obj, the reference's default shading: ground plane + Lambert + shadows + "
+                     "one reflection (raytracing.cpp:13-65)"),
+}
+EXTRAS = ["grid", "grid_shipped", "octree", "octree_shipped", "mesh_large", "default_mode"]
 
 
 def parse():
@@ -76,79 +102,123 @@ def parse():
     ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
                     help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
     ap.add_argument("--group", type=int, default=8,
-                    help="frames per launch (blockIdx.z = frame); N>1: also per completion signal / gather")
+                    help="frames per launch (at most 8); N>1: also per completion signal / gather")
     ap.add_argument("--depth", type=int, default=3, help="N>1: groups whose slots are in flight")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the launches alternate over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU sample")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="wall budget of the CPU sample")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--dist", action="store_true",
                     help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
 
 
-def host_threads() -> int:
+def host_threads():
+    """CPU threads this process may actually run on -> (threads, how it was decided).
+    The affinity set can list the whole machine while a cgroup quota (cpu.max) or
+    the job's OMP_NUM_THREADS grants a share of it (the GPU box: 256 CPUs listed,
+    16 granted); oversubscribing that share makes OpenMP far slower, so the
+    smallest of the three is used."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except Exception:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        aff = os.cpu_count() or 1
+    n, why = aff, f"affinity set {aff}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max" and int(q) // int(per) < n:
+            n, why = max(1, int(q) // int(per)), f"cgroup cpu.max quota {q}/{per} (affinity set {aff})"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, why = int(omp), f"OMP_NUM_THREADS={omp} (affinity set {aff})"
+    return max(1, n), why
 
 
-def frame_params(n_frames):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def orbit_params(n, W=W_IMG, H=H_IMG, mode="primary"):
     orbit = WL.orbit_positions(64)
-    return [WL.params_for(orbit[k % 64], W_IMG, H_IMG, rtamd.ShadingMode.Normal)
-            for k in range(n_frames)]
+    sm = rtamd.ShadingMode.Normal if mode == "primary" else rtamd.ShadingMode.Lambert
+    return [WL.params_for(orbit[k % 64], W, H, sm) for k in range(n)]
+
+
+def split_launches(k0, n, batch):
+    """n frames from k0 as ceil(n / batch) launches of near-equal size."""
+    if n <= 0:
+        return []
+    nl = -(-n // batch)
+    base, extra = divmod(n, nl)
+    out, k = [], k0
+    for j in range(nl):
+        m = base + (1 if j < extra else 0)
+        out.append((k, m))
+        k += m
+    return out
 
 
 def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG, inflight=2, tile=None, batch=1):
-    """N=1: full frames, render kernel only. Frames go out in launches of
-    `batch` frames (rt_render_device_frames: blockIdx.z = frame, so a frame's
-    silhouette tail is covered by the next frames' tiles); launch j is issued
-    on stream j % inflight with its own framebuffers, so up to `inflight`
-    launches are in flight. batch=1, inflight=1 is one frame at a time. HIP
-    events bracket each launch on its own stream.
-    Returns (wall_s, kernel_ms_avg per launch, buffers of the last frame)."""
+    """Full frames (or one rank's row bands with `tile`), render kernel only.
+    Frames go out in launches of up to `batch` frames (rt_render_device_frames);
+    launch j is issued on stream j % inflight with its own framebuffers. Before
+    t0 every stream is prepared (rt_stream_prepare) and warmed with at least one
+    full launch; params[i] is used for frame i (warm-up frames cycle through
+    params). HIP events bracket each timed launch on its own stream.
+    Returns (wall_s, per-launch kernel ms [(ms, frames)], buffers of the last frame)."""
     dev = torch.device("cuda")
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    for st in streams:
+        rtamd._lib.check(rtamd.lib().rt_stream_prepare(ctypes.c_void_p(st.cuda_stream)))
     bufs = [[(torch.empty((H, W), dtype=torch.int32, device=dev),
               torch.empty((H, W), dtype=torch.float32, device=dev)) for _ in range(batch)]
             for _ in range(inflight)]
 
-    def issue(j, k0, n, ev=None):
+    def issue(j, prm, ev=None):
         st = streams[j % inflight]
-        fb = bufs[j % inflight][:n]
+        fb = bufs[j % inflight][:len(prm)]
         with torch.cuda.stream(st):
             if ev:
                 ev[0].record(st)
-            if n == 1:
-                scene.render_device(params[k0], fb[0][0].data_ptr(), fb[0][1].data_ptr(), W, H, clear=True,
+            if len(prm) == 1:
+                scene.render_device(prm[0], fb[0][0].data_ptr(), fb[0][1].data_ptr(), W, H, clear=True,
                                     tile=tile, stream=st.cuda_stream)
             else:
-                scene.render_device_frames(params[k0:k0 + n], [c.data_ptr() for c, _ in fb],
-                                           [t.data_ptr() for _, t in fb], W, H, rtamd.RT_FLAG_CLEAR,
-                                           tile=tile, stream=st.cuda_stream)
+                scene.render_device_frames(prm, [c.data_ptr() for c, _ in fb], [t.data_ptr() for _, t in fb],
+                                           W, H, rtamd.RT_FLAG_CLEAR, tile=tile, stream=st.cuda_stream)
             if ev:
                 ev[1].record(st)
 
-    def launches(k0, nframes):
-        return [(k0 + i, min(batch, nframes - i)) for i in range(0, nframes, batch)]
-
-    for j, (k, n) in enumerate(launches(0, warmup)):
-        issue(j, k, n)
-    timed = launches(warmup, steps)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in timed]
+    nwarm = max(warmup, inflight * batch)
+    for j, (k, n) in enumerate(split_launches(0, nwarm, batch)):
+        issue(j, [params[(k + i) % len(params)] for i in range(n)])
+    timed = split_launches(warmup, steps, batch)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j, (k, n) in enumerate(timed):
-        issue(j, k, n, evs[j])
+        issue(j, params[k:k + n], evs[j])
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    launches = [(a.elapsed_time(b), n) for (a, b), (_, n) in zip(evs, timed)]
     jl, (kl, nl) = len(timed) - 1, timed[-1]
-    return wall, kms, bufs[jl % inflight][nl - 1]
+    return wall, launches, bufs[jl % inflight][nl - 1]
+
+
+def per_frame_ms(launches):
+    """Frame-weighted kernel time per frame over the timed launches."""
+    return sum(ms for ms, _ in launches) / sum(n for _, n in launches)
 
 
 def run_distributed(scene, params, warmup, steps, a):
@@ -164,7 +234,8 @@ def run_distributed(scene, params, warmup, steps, a):
     def make(exchange):
         r = RowSplitRenderer(scene, W_IMG, H_IMG, band_rows=a.band_rows, group=a.group, depth=a.depth,
                              streams=a.streams, exchange=exchange)
-        r.render(params[:max(warmup, 1)])
+        # warm every stream and slot group the timed region will use
+        r.render(params[:max(warmup, a.group * a.streams * a.depth)])
         r.drain()
         return r
 
@@ -173,8 +244,9 @@ def run_distributed(scene, params, warmup, steps, a):
     # a p2p exchange that fails this (IPC mapping, peer-store visibility) is replaced
     # by the RCCL gather before anything is timed
     ok = 1
+    nw = max(warmup, a.group * a.streams * a.depth)
     if dist.get_rank() == 0:
-        _, _, (c1, t1) = run_single(scene, params[max(warmup, 1) - 1:max(warmup, 1)], 0, 1, inflight=1)
+        _, _, (c1, t1) = run_single(scene, params[nw - 1:nw], 0, 1, inflight=1)
         fc, ft = rs.last()
         ok = int(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
     if not rs._all_ok(ok):
@@ -195,56 +267,45 @@ def run_distributed(scene, params, warmup, steps, a):
     # render-launch duration of this rank's bands: the same launches (a.group frames each,
     # a.streams streams) rendered locally, HIP events on each launch's stream
     n = min(steps, 64)
-    _, kms, _ = run_single(scene, params[warmup:warmup + n], 0, n, inflight=a.streams, tile=rs.tile,
-                           batch=a.group)
-    return wall, kms, rs
+    _, launches, _ = run_single(scene, params[warmup:warmup + n], 0, n, inflight=a.streams, tile=rs.tile,
+                                batch=a.group)
+    return wall, per_frame_ms(launches) * a.group, rs
 
 
-def roofline(scene, params, tile, kms, W=W_IMG, H=H_IMG, amortized_ms=None, frames_per_launch=1):
-    """Algorithmic bytes per launch (SURVEY.md 8(d) byte model, counted exactly
-    by the counting variant of the kernel over the same frames) / the kernel's
-    event-timed average launch duration over the timed region (kernel_ms, what
-    rocprofv3's kernel stats report). With frames in flight the launches
-    overlap; the amortized rate (wall / launches) is reported beside it."""
+def roofline(scene, params, tile, kms, frames_per_launch, W=W_IMG, H=H_IMG):
+    """algorithmic bytes per launch (counted exactly by the
+    diagnostic kernel over the same frames) / the event-timed launch duration,
+    against the HBM peak. The PMC-measured fields are added by attach_pmc()."""
     c = scene.count_work(params, W, H, clear=True, tile=tile)
     npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
     algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params) * frames_per_launch
-    if amortized_ms is not None:
-        amortized_ms *= frames_per_launch
     achieved = algo / (kms * 1e-3) / 1e9
     per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
-    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-           "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
-           "work_per_ray": per_ray, "frames_per_launch": frames_per_launch}
-    if amortized_ms is not None:
-        # launches overlap (frames in flight): algorithmic bytes per amortized launch.
-        # The byte model counts cache-served bytes, so this can exceed the HBM peak.
-        out["amortized_ms_per_launch"] = round(amortized_ms, 5)
-        out["amortized_achieved"] = round(algo / (amortized_ms * 1e-3) / 1e9, 1)
-    return out
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "basis": "algorithmic bytes (SURVEY.md 8(d) byte model on the reference's data layout); "
+                     "the scenes are cache-resident, so these bytes are served mostly by L1/L2, not DRAM",
+            "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
+            "frames_per_launch": frames_per_launch, "work_per_ray": per_ray,
+            "algorithmic_vs_l2_peak": round(achieved / L2_PEAK_GBS, 4)}
 
 
-def one_stream(scene, params, warmup, steps, W, H, group, rl):
-    """The same launches (group frames each) issued on ONE stream: launches do
-    not overlap, so the event-timed launch duration is the launch's own time
-    and bytes / duration is the kernel's rate without a second launch beside
-    it. Reported beside the default two-stream roofline."""
-    wall, kms, _ = run_single(scene, params, warmup, steps, W, H, inflight=1, batch=group)
-    achieved = rl["algorithmic_bytes_per_launch"] / (kms * 1e-3) / 1e9
-    return {"streams": 1, "ms_per_step": round(wall * 1e3 / steps, 4), "kernel_ms": round(kms, 5),
-            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4)}
+# ------------------------------------------------------------ PMC passes --
+PMC_PASSES = [
+    ["FETCH_SIZE"],
+    ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
+    ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU",
+     "SQ_INSTS_VMEM_RD", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "GRBM_GUI_ACTIVE"],
+]
+PMC_LAUNCHES = 2
 
 
-def pmc_traffic(workload, W, H, group, frames=32):
-    """HBM bytes per launch of the headline render kernel (launches of `group`
-    frames, the timed region's launch shape) from rocprofv3 PMC counters,
-    collected in two separate --pmc passes (FETCH_SIZE, WRITE_SIZE cannot
-    share a pass) over tools/prof_frames.py, as MI355X_MICROARCH.md's
-    HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-    FETCH_SIZE reports half the bytes of coalesced reads, so it is doubled.
-    Runs as child processes BEFORE this process touches the GPU. Returns
-    (bytes_per_launch | None, detail dict)."""
+def pmc_counters(keys, group):
+    """rocprofv3 --pmc passes (one counter set per run, as MI355X_MICROARCH.md
+    prescribes) over tools/prof_frames.py, which renders PMC_LAUNCHES launches
+    of `group` frames of every workload in `keys`, in order, on one stream.
+    Runs as child processes BEFORE this process touches the GPU.
+    Returns ({key: {counter: mean per launch}}, error | None)."""
     import csv
     import glob
     import shutil
@@ -252,124 +313,146 @@ def pmc_traffic(workload, W, H, group, frames=32):
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
-        return None, {"error": "rocprofv3 not found"}
+        return {}, "rocprofv3 not found"
     env = dict(os.environ, TMPDIR="/tmp")
-    vals = {}
-    # the batch path's kernel: render_persist_kernel (work queue) or, with
-    # RTAMD_PERSIST=0, render_batch_kernel; one frame per launch: render_kernel
-    knames = ("render_persist_kernel", "render_batch_kernel") if group > 1 else ("render_kernel",)
+    plan = ",".join(f"{k}:{WORKLOADS[k][0]}:{WORKLOADS[k][1]}:{WORKLOADS[k][2]}:{WORKLOADS[k][3]}" for k in keys)
+    out = {k: {} for k in keys}
     tmp = tempfile.mkdtemp(prefix="rtamd_pmc_", dir="/tmp")
     try:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            d = os.path.join(tmp, ctr)
-            cmd = ["timeout", "-k", "10", "180", prof, "--pmc", ctr, "--output-format", "csv", "-d", d,
+        for i, ctrs in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, f"p{i}")
+            cmd = ["timeout", "-k", "10", "240", prof, "--pmc", *ctrs, "--output-format", "csv", "-d", d,
                    "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_frames.py"),
-                   "--workload", workload, "--frames", str(frames), "--W", str(W), "--H", str(H),
-                   "--group", str(group)]
+                   "--plan", plan, "--group", str(group), "--launches", str(PMC_LAUNCHES)]
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
             if r.returncode != 0:
-                return None, {"error": f"{ctr} pass rc={r.returncode}: {r.stderr[-300:]}"}
-            per = []
+                return out, f"pass {ctrs} rc={r.returncode}: {r.stderr[-300:]}"
+            rows = {}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if any(k in row["Kernel_Name"] for k in knames) and row["Counter_Name"] == ctr:
-                            per.append(float(row["Counter_Value"]))
-            if not per:
-                return None, {"error": f"no {ctr} rows for {knames}"}
-            vals[ctr] = sum(per) / len(per)
+                        if "render_" not in row["Kernel_Name"]:
+                            continue
+                        rows.setdefault(int(row["Dispatch_Id"]), {})[row["Counter_Name"]] = \
+                            float(row["Counter_Value"])
+            disp = [rows[k] for k in sorted(rows)]
+            if len(disp) != PMC_LAUNCHES * len(keys):
+                return out, f"pass {ctrs}: {len(disp)} render dispatches, expected {PMC_LAUNCHES * len(keys)}"
+            for j, k in enumerate(keys):
+                mine = disp[j * PMC_LAUNCHES:(j + 1) * PMC_LAUNCHES]
+                for c in ctrs:
+                    out[k][c] = sum(m.get(c, 0.0) for m in mine) / len(mine)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
-    write = vals["WRITE_SIZE"] * 1024.0
-    return fetch + write, {"fetch_bytes": round(fetch), "write_bytes": round(write),
-                           "raw_kib": {k: round(v, 1) for k, v in vals.items()},
-                           "launches": frames // group, "frames_per_launch": group,
-                           "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
+    return out, None
 
 
-def standin_scenes(which):
-    """BASELINE configs 3-5 stand-ins, generated deterministically on the GPU
-    from the shipped stanford-bunny.obj (rt_sdf_mesh_* / rt_mesh_subdivide)."""
-    from rtamd import data
-    bunny = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
-    if which == "mesh_large":
-        return rtamd.BVHBuilder(rtamd.subdivide_mesh(bunny, 2))
-    sm = rtamd.SDFMesh(bunny)
-    if which == "grid":
-        return rtamd.SDFGrid(*sm.grid(256))
-    return rtamd.SDFOctree(sm.octree(8))
+def attach_pmc(rl, ctr, err):
+    """Add the counter-derived roofs to a roofline dict (per launch of the same shape)."""
+    if err or not ctr or "FETCH_SIZE" not in ctr or "SQ_INSTS_VALU" not in ctr:
+        rl["pmc_error"] = err or "no counters"
+        return rl
+    fetch = 2.0 * ctr["FETCH_SIZE"] * 1024.0  # gfx950: FETCH_SIZE reports half of the bytes; KiB -> B
+    write = ctr["WRITE_SIZE"] * 1024.0
+    dur = rl["kernel_ms"] * 1e-3
+    rl["traffic"] = round(fetch + write)
+    dram_gbs = (fetch + write) / dur / 1e9
+    valu = ctr["SQ_INSTS_VALU"]
+    issue2 = valu * 2.0 / (SIMDS * CLOCK_HZ * dur)
+    issue4 = valu * 4.0 / (SIMDS * CLOCK_HZ * dur)
+    hits, miss = ctr.get("TCC_HIT_sum", 0.0), ctr.get("TCC_MISS_sum", 0.0)
+    rl["dram"] = {"fetch_bytes": round(fetch), "write_bytes": round(write), "achieved": round(dram_gbs, 1),
+                  "frac": round(dram_gbs / HBM_PEAK_GBS, 4),
+                  "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
+    rl["valu_issue"] = {"insts_per_launch": round(valu), "frac": round(issue2, 4),
+                        "frac_4cyc": round(issue4, 4),
+                        "model": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x 2.4 GHz x "
+                                 "launch duration); frac_4cyc: the single-wave 4-cycle issue cost"}
+    rl["l2"] = {"hit_rate": round(hits / (hits + miss), 4) if hits + miss else None,
+                "tcp_to_tcc_read_req": round(ctr.get("TCP_TCC_READ_REQ_sum", 0.0)),
+                "tcp_accesses": round(ctr.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0))}
+    rl["sq"] = {k: round(ctr[k]) for k in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU",
+                                           "SQ_INSTS_VMEM_RD", "GRBM_GUI_ACTIVE") if k in ctr}
+    roofs = {"dram": rl["dram"]["frac"], "valu_issue": issue2, "algorithmic_vs_l2": rl["algorithmic_vs_l2_peak"]}
+    top = max(roofs, key=roofs.get)
+    rl["binding"] = top if roofs[top] >= 0.5 else \
+        f"latency: no throughput roof above {roofs[top]:.2f} (largest: {top})"
+    return rl
 
 
-EXTRAS = [
-    # key, scene source, W, H, description
-    ("grid", "grid", 1920, 1080,
-     "stanford-bunny SDF 256^3 grid generated on the GPU (stand-in for the missing "
-     "example_grid_large.grid, BASELINE configs[2])"),
-    ("grid_shipped", "example_grid.grid", 1920, 1080, "shipped example_grid.grid (65^3)"),
-    ("octree", "octree", 3840, 2160,
-     "stanford-bunny SDF octree of depth 8 generated on the GPU (stand-in for the missing "
-     "example_octree_large.octree, BASELINE configs[3])"),
-    ("octree_shipped", "sdf_6.octree", 3840, 2160, "shipped sdf_6.octree"),
-    ("mesh_large", "mesh_large", 3840, 2160,
-     "stanford-bunny midpoint-subdivided twice, 1,111,216 triangles (stand-in for the missing "
-     "MotorcycleCylinderHead.obj, BASELINE configs[4]), 1 GPU"),
-]
-
-
-def run_extras(warmup, steps, streams, group):
-    out = {}
-    for key, src, W, H, desc in EXTRAS:
-        if "." in src:
-            kind, payload, _ = WL.load_input(src)
-            sc = WL.make_scene(kind, payload)
-        else:
-            sc = standin_scenes(src)
-        sc.set_plane(None)
-        orbit = WL.orbit_positions(64)
-        prm = [WL.params_for(orbit[k % 64], W, H, rtamd.ShadingMode.Normal) for k in range(warmup + steps)]
-        wall, kms, _ = run_single(sc, prm, warmup, steps, W, H, inflight=streams, batch=group)
-        rl = roofline(sc, prm[warmup:], None, kms, W, H, wall * 1e3 / steps, group)
-        out[key] = {"workload": f"{desc}, {W}x{H} primary rays, same orbit",
-                    "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
-                    "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps, "roofline": rl}
-        if streams > 1:
-            out[key]["roofline_one_stream"] = one_stream(sc, prm, warmup, steps, W, H, group, rl)
-        sc.close()
-        torch.cuda.synchronize()
+# ------------------------------------------------------------ workloads --
+def measure(key, warmup, steps, streams, group, pmc, pmc_err, scene=None):
+    src, W, H, mode, desc = WORKLOADS[key]
+    own = scene is None
+    if own:
+        scene, off = WL.scene_for(src)
+    else:
+        off = None
+    if mode == "default":
+        if off is None:
+            off = WL.load_input(src)[2]
+        scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off))
+    else:
+        scene.set_plane(None)
+    prm = orbit_params(warmup + steps, W, H, mode)
+    wall, launches, _ = run_single(scene, prm, warmup, steps, W, H, inflight=streams, batch=group)
+    kms = per_frame_ms(launches) * group
+    rl = attach_pmc(roofline(scene, prm[warmup:], None, kms, group, W, H), pmc.get(key), pmc_err)
+    amort = [ms / n for ms, n in launches]
+    out = {"workload": f"{desc}, {W}x{H}, {'primary rays (Normal shading, no plane)' if mode == 'primary' else 'default mode'}, "
+                       "same orbit",
+           "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
+           "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
+           "kernel_ms_per_frame": {"mean": round(per_frame_ms(launches), 5),
+                                   "p50": round(statistics.median(amort), 5)},
+           "roofline": rl}
+    if mode == "default":
+        rays = rl["work_per_ray"].get("rays", 1.0)
+        out["traced_rays_per_pixel"] = rays
+        out["traced_value"] = round(W * H * rays * steps / wall / 1e6, 1)
+        out["value_note"] = ("value = primary rays (pixels) per second; traced_value counts every ray the "
+                             "frame traces (primary + shadow + reflection + reflection shadow)")
+    if streams > 1:  # the same launches on ONE stream: a launch's duration is its own
+        w1, l1, _ = run_single(scene, prm, warmup, steps, W, H, inflight=1, batch=group)
+        k1 = per_frame_ms(l1) * group
+        a1 = rl["algorithmic_bytes_per_launch"] / (k1 * 1e-3) / 1e9
+        out["one_stream"] = {"ms_per_step": round(w1 * 1e3 / steps, 4), "kernel_ms": round(k1, 5),
+                             "achieved": round(a1, 1), "frac": round(a1 / HBM_PEAK_GBS, 4)}
+    if own:
+        scene.close()
+    torch.cuda.synchronize()
     return out
 
 
-def cpu_baseline(name, budget_s):
+def cpu_baseline(name, budget_s, mode="primary", max_frames=64):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpuref  # the oracle: test infrastructure, used here only as the CPU baseline
     from rtamd import data
     p = data.path(name)
-    threads = host_threads()
-    if name.endswith(".obj"):
-        v, i = cpuref.load_obj(p)
-        sc = cpuref.RefScene.mesh(v, i)
+    threads, why = host_threads()
+    v, i = cpuref.load_obj(p)
+    sc = cpuref.RefScene.mesh(v, i)
+    if mode == "default":
+        sc.set_plane(True, (0.0, 1.0, 0.0), float((v[:, 1] / v[:, 3]).min()))
     else:
-        import numpy as np
-        size = np.fromfile(p, np.uint32, 3)
-        vals = np.fromfile(p, np.float32, offset=12)
-        sc = cpuref.RefScene.grid(size, vals)
-    sc.set_plane(False)
+        sc.set_plane(False)
     orbit = WL.orbit_positions(64)
     frames, ms_total = 0, 0.0
     t0 = time.perf_counter()
-    while frames < 64 and (time.perf_counter() - t0) < budget_s:
-        vi, pi = cpuref.camera_matrices(orbit[frames], aspect=W_IMG / H_IMG)
-        P = cpuref.make_params(orbit[frames], vi, pi, mode=0)
+    while frames < max_frames and (time.perf_counter() - t0) < budget_s:
+        vi, pi = cpuref.camera_matrices(orbit[frames % 64], aspect=W_IMG / H_IMG)
+        P = cpuref.make_params(orbit[frames % 64], vi, pi, mode=0 if mode == "primary" else 1)
         _, _, _, ms = sc.render(P, W_IMG, H_IMG, threads=threads)
         ms_total += ms
         frames += 1
     mrays = W_IMG * H_IMG * frames / (ms_total * 1e-3) / 1e6
     return {"value": round(mrays, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "ms_per_frame": round(ms_total / frames, 2),
-            "sample": f"{frames} frames of the 64-frame orbit, {name} {W_IMG}x{H_IMG} primary rays, "
-                      f"OpenMP schedule(dynamic) over rows, {threads} threads, ISPC kernels as scalar "
-                      f"C++ (oracle/cpuref.cpp)"}
+            "ms_per_frame": round(ms_total / frames, 2), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "threads_from": why,
+            "sample": f"{frames} frames of the 64-frame orbit, {name} {W_IMG}x{H_IMG} "
+                      f"{'primary rays' if mode == 'primary' else 'default mode (plane + Lambert + shadows + reflection)'}, "
+                      f"OpenMP schedule(dynamic) over rows on {threads} threads ({why}), timed "
+                      f"around the pixel loop as Renderer::draw does; ISPC kernels as scalar C++ (oracle/cpuref.cpp)"}
 
 
 def main():
@@ -378,17 +461,20 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     a = parse()
+    if not 1 <= a.group <= 8:
+        raise SystemExit("--group must be 1..8 (frames per launch)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     use_dist = world > 1 or a.dist
-    pmc, pmc_extra = None, {}
+    headline = "bunny" if a.workload == "stanford-bunny.obj" else None
+    pmc, pmc_err = {}, "skipped (--no-pmc or N>1)"
     if not use_dist and not a.no_pmc:
-        pmc = pmc_traffic(a.workload, W_IMG, H_IMG, a.group)  # child processes, before this one inits the GPU
-        if not a.no_extra:  # the SDF-grid sphere march (north star: >= 60 % of HBM peak)
-            pmc_extra["grid"] = pmc_traffic("grid", W_IMG, H_IMG, a.group)
+        keys = ([headline] if headline else []) + ([] if a.no_extra else EXTRAS)
+        if keys:  # child processes, before this one initialises the GPU
+            pmc, pmc_err = pmc_counters(keys, a.group)
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
@@ -409,37 +495,42 @@ def main():
     kind, payload, _ = WL.load_input(a.workload)
     scene = WL.make_scene(kind, payload)
     scene.set_plane(None)
-    params = frame_params(a.warmup + a.steps)
+    params = orbit_params(max(a.warmup + a.steps, a.group * a.streams * a.depth))
 
     latency = None
     if not use_dist:
-        wall, kms, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.streams, batch=a.group)
+        wall, launches, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.streams, batch=a.group)
+        kms = per_frame_ms(launches) * a.group
+        amort = [ms / n for ms, n in launches]
         tile = None
-        if a.streams * a.group > 1:  # single-frame latency (one frame at a time), reported beside
-            lwall, lkms, _ = run_single(scene, params, min(a.warmup, 8), min(a.steps, 64), inflight=1)
-            latency = {"ms_per_frame": round(lwall * 1e3 / min(a.steps, 64), 4),
-                       "kernel_ms": round(lkms, 5)}
+        if a.streams * a.group > 1:  # one frame at a time (latency), reported beside
+            nl = min(a.steps, 64)
+            lwall, ll, _ = run_single(scene, params, min(a.warmup, 8), nl, inflight=1)
+            lat = [ms for ms, _ in ll]
+            latency = {"ms_per_frame": round(lwall * 1e3 / nl, 4), "kernel_ms_mean": round(statistics.mean(lat), 5),
+                       "kernel_ms_p50": round(statistics.median(lat), 5), "frames": nl}
     else:
         wall, kms, rs = run_distributed(scene, params, a.warmup, a.steps, a)
         tile = rs.tile
-        t = torch.tensor([wall], dtype=torch.float64,
-                         device="cpu" if dist.get_backend() == "gloo" else "cuda")
+        dev_t = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        t = torch.tensor([wall], dtype=torch.float64, device=dev_t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
+        kall = torch.zeros(world, dtype=torch.float64, device=dev_t)
+        kall[rank] = kms
+        dist.all_reduce(kall, op=dist.ReduceOp.SUM)
+        rank_kms = [round(float(x), 5) for x in kall.cpu()]
         if rank == 0:  # the assembled last frame must equal a whole-frame render of it
-            _, _, (c1, t1) = run_single(scene, params[-1:], 0, 1, inflight=1)
+            _, _, (c1, t1) = run_single(scene, params[a.warmup + a.steps - 1:a.warmup + a.steps], 0, 1, inflight=1)
             fc, ft = rs.last()
             check_equal = bool(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
         dist.barrier()
         rs.close()
 
-    rl = roofline(scene, params[a.warmup:], tile, kms, amortized_ms=wall * 1e3 / a.steps,
-                  frames_per_launch=a.group)
-    if pmc is not None:
-        rl["traffic"] = None if pmc[0] is None else round(pmc[0])
-        rl["traffic_detail"] = pmc[1]
-    total_rays = W_IMG * H_IMG * a.steps
-    value = total_rays / wall / 1e6
+    rl = roofline(scene, params[a.warmup:a.warmup + a.steps], tile, kms, a.group)
+    if headline and not use_dist:
+        attach_pmc(rl, pmc.get(headline), pmc_err)
+    value = W_IMG * H_IMG * a.steps / wall / 1e6
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
@@ -454,22 +545,34 @@ def main():
                    "frames_per_launch": a.group, "streams": a.streams},
         "roofline": rl,
     }
+    if not use_dist:
+        out["kernel_ms_per_frame"] = {"mean": round(per_frame_ms(launches), 5),
+                                      "p50": round(statistics.median(amort), 5)}
     if latency is not None:
         out["frame_latency"] = latency
     if not use_dist and a.streams > 1:
-        out["roofline_one_stream"] = one_stream(scene, params, a.warmup, a.steps, W_IMG, H_IMG, a.group, rl)
+        w1, l1, _ = run_single(scene, params, a.warmup, a.steps, inflight=1, batch=a.group)
+        k1 = per_frame_ms(l1) * a.group
+        a1 = rl["algorithmic_bytes_per_launch"] / (k1 * 1e-3) / 1e9
+        out["roofline_one_stream"] = {"streams": 1, "ms_per_step": round(w1 * 1e3 / a.steps, 4),
+                                      "kernel_ms": round(k1, 5), "achieved": round(a1, 1),
+                                      "frac": round(a1 / HBM_PEAK_GBS, 4)}
+    if use_dist:
+        out["rank_kernel_ms"] = {"per_rank": rank_kms, "max": max(rank_kms),
+                                 "note": "render-kernel ms per launch of this rank's bands "
+                                         f"({a.group} frames, {a.streams} streams); the max bounds the scaling"}
     if use_dist and rank == 0:
         out["frame_check"] = {"assembled_equals_single_render": check_equal,
                               "backend": dist.get_backend(), "exchange": rs.exchange,
                               "fallback": getattr(rs, "fallback", None)}
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_extra:
-        out["extra"] = run_extras(min(a.warmup, 16), min(a.steps, 64), a.streams, a.group)
-        for key, (tb, detail) in pmc_extra.items():
-            out["extra"][key]["roofline"]["traffic"] = None if tb is None else round(tb)
-            out["extra"][key]["roofline"]["traffic_detail"] = detail
+        out["extra"] = {k: measure(k, min(a.warmup, 16), min(a.steps, 64), a.streams, a.group, pmc, pmc_err)
+                        for k in EXTRAS}
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
+        if not a.no_extra:
+            out["cpu_baseline"]["default_mode"] = cpu_baseline(a.workload, a.cpu_seconds / 3, "default", 16)
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if use_dist:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 3
+#define RTAMD_ABI_VERSION 4
 
 enum rt_status {
   RT_OK = 0,
@@ -168,6 +168,15 @@ int rt_render_device_frames(rt_scene *s, const rt_render_params *params, int32_t
 /* FrameBuffer::clear() (src/raytracing.hpp:16-19) on device buffers: color = 0,
  * t = +inf over n pixels, on `stream`. */
 int rt_clear_device(uint32_t *d_color, float *d_t, int64_t n, void *stream);
+/* Per-stream render state (the multi-frame launches' work-queue heads),
+ * allocated and zeroed in stream order on the current device. Optional:
+ * rt_render_device_frames creates it on a stream's first use, also in stream
+ * order (no device-wide synchronisation); calling this first keeps that
+ * allocation out of a timed region. rt_stream_release frees it (stream
+ * ordered); a later launch on the stream re-creates it. No reference
+ * counterpart: the reference renders on the host (src/raytracing.cpp:67-102). */
+int rt_stream_prepare(void *stream);
+int rt_stream_release(void *stream);
 
 /* ---- frame exchange over xGMI (multi-GPU, one process per GPU) -----------
  * Rank 0 allocates its frame slots with rt_exchange_alloc, exports them with

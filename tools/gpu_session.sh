@@ -1,0 +1,25 @@
+#!/bin/bash
+# One gpurun session: GPU tests, the driver's bench command, a long bench run and a
+# rocprofv3 kernel-stats pass. usage (on the box): tools/gpu_session.sh OUT [steps...]
+#   steps: tests | fulltests | bench | bench128 | prof | split
+# Every GPU step runs under its own timeout; the first failure ends the session.
+set -o pipefail
+OUT=${1:-gpurun_out/s}; shift
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+run() { local name=$1 secs=$2; shift 2
+  echo "== $name: $*"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
+  echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"; return $rc; }
+for step in "$@"; do
+  case $step in
+    tests) run tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not fullsize" || exit 1 ;;
+    fulltests) run fulltests 600 python -u -m pytest tests/test_fullsize.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench) run bench 900 python bench.py --gpus 1 --steps 20 --warmup 5 && tail -1 "$OUT/bench.log" > "$OUT/bench.json" || exit 1 ;;
+    bench128) run bench128 600 python bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline --no-extra && tail -1 "$OUT/bench128.log" > "$OUT/bench128.json" || exit 1 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o p -- python3 bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline || exit 1 ;;
+    split) run split 600 python tools/ab.py split bunny || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== session done"

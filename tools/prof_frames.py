@@ -1,41 +1,67 @@
-"""Render N orbit frames of one workload back to back (profiling driver)."""
+"""Render orbit frames of one or more workloads back to back (profiling driver).
+
+Run under `rocprofv3 --pmc ...` by bench.py (one process per counter pass, all
+workloads in it) and by hand. Every workload issues exactly `--launches`
+launches of `--group` frames on ONE stream (the bench's launch shape; counters
+are per dispatch), in the order given, so a reader can map the render-kernel
+dispatches to workloads by dispatch order.
+
+--plan key:src:W:H:mode[,key:src:W:H:mode...]  (src: a shipped input file or a
+stand-in key of rtamd.workloads.STANDINS; mode: primary | default)
+"""
 import argparse
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd"))
-import torch  # noqa: F401,E402  (one HIP runtime)
+import torch  # noqa: E402  (one HIP runtime)
 import rtamd  # noqa: E402
 from rtamd import workloads as WL  # noqa: E402
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--workload", default="stanford-bunny.obj")
-ap.add_argument("--frames", type=int, default=16)
-ap.add_argument("--W", type=int, default=1920)
-ap.add_argument("--H", type=int, default=1080)
-ap.add_argument("--mode", default="primary")
-ap.add_argument("--group", type=int, default=1, help="frames per launch (bench.py's --group)")
-a = ap.parse_args()
-if a.workload in ("grid", "octree", "mesh_large"):  # bench.py's generated stand-ins
-    sys.path.insert(0, ROOT)
-    import bench  # noqa: E402
-    s, off = bench.standin_scenes(a.workload), -1.0
-else:
-    kind, payload, off = WL.load_input(a.workload)
-    s = WL.make_scene(kind, payload)
-if a.mode == "primary":
-    s.set_plane(None)
-    P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Normal) for p in WL.orbit_positions(64)]
-else:
-    s.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off))
-    P = [WL.params_for(p, a.W, a.H, rtamd.ShadingMode.Lambert) for p in WL.orbit_positions(64)]
-frames = [P[k % 64] for k in range(a.frames)]
-if a.group > 1:  # the bench's launch shape: `group` frames per launch (one stream: counters are per dispatch)
-    sys.path.insert(0, ROOT)
-    import bench  # noqa: E402
-    wall, kms, _ = bench.run_single(s, frames, 0, a.frames, a.W, a.H, inflight=1, batch=a.group)
-    print(f"{a.workload} {a.W}x{a.H} {a.mode}: {kms:.4f} ms/launch of {a.group} frames", flush=True)
-else:
-    mean, total = s.bench_frames(frames, a.W, a.H)
-    print(f"{a.workload} {a.W}x{a.H} {a.mode}: {mean:.4f} ms/frame", flush=True)
+
+def frames_for(W, H, mode, n):
+    orbit = WL.orbit_positions(64)
+    sm = rtamd.ShadingMode.Normal if mode == "primary" else rtamd.ShadingMode.Lambert
+    return [WL.params_for(orbit[k % 64], W, H, sm) for k in range(n)]
+
+
+def run(src, W, H, mode, group, launches):
+    s, off = WL.scene_for(src)
+    s.set_plane(None if mode == "primary" else rtamd.Plane((0.0, 1.0, 0.0), off))
+    P = frames_for(W, H, mode, group * launches)
+    dev = torch.device("cuda")
+    st = torch.cuda.current_stream()
+    bufs = [(torch.empty((H, W), dtype=torch.int32, device=dev), torch.empty((H, W), dtype=torch.float32, device=dev))
+            for _ in range(group)]
+    rtamd.lib().rt_stream_prepare(st.cuda_stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(st)
+    for j in range(launches):
+        fr = P[j * group:(j + 1) * group]
+        if group == 1:
+            s.render_device(fr[0], bufs[0][0].data_ptr(), bufs[0][1].data_ptr(), W, H, clear=True,
+                            stream=st.cuda_stream)
+        else:
+            s.render_device_frames(fr, [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs], W, H,
+                                   rtamd.RT_FLAG_CLEAR, stream=st.cuda_stream)
+    ev[1].record(st)
+    torch.cuda.synchronize()
+    s.close()
+    return ev[0].elapsed_time(ev[1]) / launches
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--plan", default="bunny:stanford-bunny.obj:1920:1080:primary")
+    ap.add_argument("--group", type=int, default=8)
+    ap.add_argument("--launches", type=int, default=2)
+    a = ap.parse_args()
+    for item in a.plan.split(","):
+        key, src, W, H, mode = item.split(":")
+        ms = run(src, int(W), int(H), mode, a.group, a.launches)
+        print(f"{key} ({src} {W}x{H} {mode}): {ms:.4f} ms per launch of {a.group} frames", flush=True)
+
+
+if __name__ == "__main__":
+    main()

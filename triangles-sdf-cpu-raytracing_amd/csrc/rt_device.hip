@@ -884,25 +884,35 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
 // Work-queue heads of render_persist_kernel, one set per (device, stream):
 // launches on one stream run in order, and each launch's last wave resets its
 // heads, so consecutive launches on a stream reuse them; concurrent streams
-// never share a set.
+// never share a set. The set is allocated and zeroed IN STREAM ORDER
+// (hipMallocAsync + hipMemsetAsync on that stream): no device-wide sync, so a
+// first launch on a new stream neither stalls the other streams nor breaks a
+// graph capture. rt_stream_prepare() does it ahead of time (outside a timed
+// region); rt_stream_release() frees the set, again in stream order.
+constexpr size_t kQueueBytes = (8 * kHeadStrideMax + 16) * sizeof(uint32_t);
 std::mutex g_queue_mu;
 std::map<std::pair<int, hipStream_t>, uint32_t *> g_queues;
 
-uint32_t *stream_queue(hipStream_t stream) {
+int stream_queue(hipStream_t stream, uint32_t **out) {
+  *out = nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  HIP_TRY(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_queue_mu);
   auto it = g_queues.find({dev, stream});
-  if (it != g_queues.end()) return it->second;
+  if (it != g_queues.end()) {
+    *out = it->second;
+    return RT_OK;
+  }
   void *p = nullptr;
-  if (hipMalloc(&p, (8 * kHeadStrideMax + 16) * sizeof(uint32_t)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, (8 * kHeadStrideMax + 16) * sizeof(uint32_t)) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
+  HIP_TRY(hipMallocAsync(&p, kQueueBytes, stream));
+  const hipError_t e = hipMemsetAsync(p, 0, kQueueBytes, stream);
+  if (e != hipSuccess) {
+    (void)hipFreeAsync(p, stream);
+    return set_err(RT_E_DEVICE, std::string("work-queue init: ") + hipGetErrorString(e));
   }
   g_queues[{dev, stream}] = (uint32_t *)p;
-  return (uint32_t *)p;
+  *out = (uint32_t *)p;
+  return RT_OK;
 }
 
 // RTAMD_PERSIST=0 selects the one-block-per-16x16-tile dispatch (A/B switch).
@@ -939,8 +949,8 @@ int launch_persist_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int 
     blocks = std::max(1, per_cu) * std::max(1, cus);
     dev_cached = dev;
   }
-  uint32_t *heads = stream_queue(stream);
-  if (!heads) return set_err(RT_E_DEVICE, "work-queue allocation failed");
+  uint32_t *heads = nullptr;
+  if (const int rc = stream_queue(stream, &heads)) return rc;
   PersistQ q;
   q.heads = heads;
   static const uint32_t stride = [] {
@@ -1385,6 +1395,26 @@ int rt_clear_device(uint32_t *d_color, float *d_t, int64_t n, void *stream) {
   const int64_t lanes = (n + 3) / 4;
   clear_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, (hipStream_t)stream>>>(d_color, d_t, n);
   HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_stream_prepare(void *stream) {
+  uint32_t *heads = nullptr;
+  return stream_queue((hipStream_t)stream, &heads);
+}
+
+int rt_stream_release(void *stream) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  uint32_t *p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_queue_mu);
+    auto it = g_queues.find({dev, (hipStream_t)stream});
+    if (it == g_queues.end()) return RT_OK;
+    p = it->second;
+    g_queues.erase(it);
+  }
+  HIP_TRY(hipFreeAsync(p, (hipStream_t)stream));
   return RT_OK;
 }
 

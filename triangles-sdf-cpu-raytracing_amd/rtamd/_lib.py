@@ -87,6 +87,8 @@ _SIGS = {
     "rt_render_device_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                           C.c_int32, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "rt_clear_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "rt_stream_prepare": (C.c_int, [C.c_void_p]),
+    "rt_stream_release": (C.c_int, [C.c_void_p]),
     "rt_exchange_alloc": (C.c_int, [C.c_int64, C.POINTER(C.c_void_p)]),
     "rt_exchange_free": (C.c_int, [C.c_void_p]),
     "rt_ipc_get_handle": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -123,9 +125,13 @@ EXPORTED = tuple(_SIGS)
 
 
 def build(force: bool = False) -> str:
-    """Compile librtamd.so in-tree (hipcc, gfx950)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", PKG_ROOT, "-s"], check=True)
+    """Compile librtamd.so in-tree (hipcc, gfx950). Always runs make: it skips
+    up-to-date targets, and the objects list their headers, so a source edit
+    never leaves a stale library behind the tests. A library injected through
+    RTAMD_LIB is taken as is."""
+    if os.environ.get("RTAMD_LIB"):
+        return LIB_PATH
+    subprocess.run(["make", "-C", PKG_ROOT, "-s"] + (["-B"] if force else []), check=True)
     return LIB_PATH
 
 

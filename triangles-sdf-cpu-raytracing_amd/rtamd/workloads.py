@@ -46,3 +46,41 @@ def make_scene(kind: str, payload):
         size, vals = payload
         return api.SDFGrid(size, vals)
     return api.SDFOctree(payload)
+
+
+STANDINS = {
+    # BASELINE configs 3-5 name inputs missing from the reference (.MISSING_LARGE_BLOBS);
+    # deterministic stand-ins generated from the shipped stanford-bunny.obj
+    "grid": "stanford-bunny SDF on a 256^3 lattice, generated on the GPU "
+            "(stand-in for example_grid_large.grid, BASELINE configs[2])",
+    "octree": "stanford-bunny SDF octree of depth 8, generated on the GPU "
+              "(stand-in for example_octree_large.octree, BASELINE configs[3])",
+    "mesh_large": "stanford-bunny midpoint-subdivided twice, 1,111,216 triangles "
+                  "(stand-in for MotorcycleCylinderHead.obj, BASELINE configs[4])",
+}
+
+
+def standin_scene(which: str):
+    """The config 3-5 stand-ins (rt_sdf_mesh_* / rt_mesh_subdivide) as scenes."""
+    bunny = api.load_mesh_from_obj(data.path("stanford-bunny.obj"))
+    if which == "mesh_large":
+        return api.BVHBuilder(api.subdivide_mesh(bunny, 2))
+    sm = api.SDFMesh(bunny)
+    try:
+        if which == "grid":
+            return api.SDFGrid(*sm.grid(256))
+        if which == "octree":
+            return api.SDFOctree(sm.octree(8))
+    finally:
+        sm.close()
+    raise ValueError(which)
+
+
+def scene_for(src: str):
+    """-> (scene, plane offset) for a shipped input file name or a stand-in key."""
+    if src in STANDINS:
+        return standin_scene(src), (-1.0 if src != "mesh_large" else
+                                    float(api.load_mesh_from_obj(data.path("stanford-bunny.obj"))
+                                          .vPos4f[:, 1].min()))
+    kind, payload, off = load_input(src)
+    return make_scene(kind, payload), off
