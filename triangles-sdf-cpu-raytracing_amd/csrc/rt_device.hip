@@ -476,6 +476,19 @@ struct PersistQ {
   uint32_t waves;    // waves in the grid
   uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
   uint32_t stride;   // words between heads
+  // diagnostic (rtx_set_persist_stamps; NULL in normal launches): per wave
+  // w = blockIdx.x * 4 + wave, 4 x u64 = start, end (s_memrealtime, 100 MHz),
+  // items traced, end of its last item
+  unsigned long long *stamps;
+  // cost-ordered queue (queue_order; NULL = frame-major natural order): item i
+  // is tile order[i / nframes] of frame i % nframes, so the tiles that were
+  // slowest in the previous launch on this stream start first in every frame
+  // and the launch's tail is made of light tiles; cost[r] collects each tile's
+  // slowest item (shader cycles) of this launch for the next one.
+  const uint32_t *order;
+  uint32_t *cost;
+  uint32_t nframes;
+  uint32_t interleave;  // frames interleaved in natural tile order (no costs): item i = tile i / nframes of frame i % nframes
 };
 // 4 KiB + 256 B apart: every head on its own memory channel's lines, so the
 // memory-side atomics of different heads do not queue behind each other
@@ -495,6 +508,9 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   const int lane = threadIdx.x & 63;
   const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
+  const unsigned long long t_start = q.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  unsigned long long t_item = t_start;
+  uint32_t n_items = 0;
   uint32_t h = xcc;
   uint32_t k = q_claim(q.heads + h * q.stride);
   NoCnt cnt{};
@@ -515,18 +531,242 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
       continue;
     }
     const uint32_t knext = q_claim(q.heads + h * q.stride);
-    const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
+    uint32_t f, r;
+    if (q.order || q.interleave) {
+      const uint32_t rank = item / q.nframes;
+      f = item - rank * q.nframes;
+      r = q.order ? q.order[rank] : rank;
+    } else {
+      f = item / q.per_frame;
+      r = item - f * q.per_frame;
+    }
+    const uint64_t c0 = q.cost ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
     for (uint32_t j = 0; j < q.gy; ++j)
       for (uint32_t i = 0; i < q.gx; ++i)
         render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[f], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
                                             (int)((ty * q.gy + j) * 8) + (lane >> 3));
+    if (q.cost) {
+      const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
+      if (lane == 0) atomicMax(q.cost + r, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt);
+    }
+    if (q.stamps) {
+      ++n_items;
+      t_item = __builtin_amdgcn_s_memrealtime();
+    }
     k = knext;
+  }
+  if (q.stamps && lane == 0) {
+    const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    q.stamps[4 * w] = t_start;
+    q.stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    q.stamps[4 * w + 2] = n_items | ((unsigned long long)xcc << 32);
+    q.stamps[4 * w + 3] = t_item;
   }
   if (lane == 0) {
     uint32_t *done = q.heads + 8 * q.stride;
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
       // every wave has left its claim loop: no claim is in flight any more
+      for (int i = 0; i < 8; ++i)
+        __hip_atomic_store(q.heads + i * q.stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- ray pump --
+// render_pump_kernel: the persistent multi-frame kernel with wavefront
+// active-ray compaction (north star: "ballot/prefix-sum active-ray compaction
+// for the sphere-march and octree steps", replacing the 8-wide ISPC gangs of
+// ray_pack.ispc:241-273 and the recursion of octree_raytracing.cpp:166-202).
+// A wave does not own a fixed 8x8 tile: each lane owns ONE ray at a time, and
+// the wave pulls pixels from a per-wave pixel stream (consecutive pixels of
+// the work-queue items, 8x8 tiles in order, so a refill's rays are coherent).
+// The traversal of every live lane runs until `refill_min` lanes have
+// finished (__ballot of the lanes still in the loop); the wave then writes the
+// finished lanes' pixels, hands each dead lane the next pixel of the stream
+// (its rank in the dead-lane ballot, __mbcnt, is its offset in the stream) and
+// resumes. Traversal state stays in the lane's registers and its own LDS stack
+// column, so nothing moves. Once the queue is drained the remaining rays run
+// to the end. Primary rays (Normal shading, no plane); every image is the
+// same as render_kernel's, bit for bit.
+struct PumpFrame {  // the per-frame arguments a lane needs, copied to LDS
+  float o[3];
+  float proj_inv[16];
+  float view_inv[16];
+  uint32_t *color;
+  float *t;
+};
+
+// wave-uniform work-item stream over the sharded queue (render_persist_kernel's
+// protocol): the ticket of the next item on head h is claimed one ahead
+struct ItemStream {
+  uint32_t h, k;
+};
+__device__ __forceinline__ uint32_t take_item(const PersistQ &q, ItemStream &s, uint32_t xcc, int lane) {
+  for (;;) {
+    const uint32_t item = s.k * 8 + s.h;
+    if (item < q.items) {
+      s.k = q_claim(q.heads + s.h * q.stride);
+      return item;
+    }
+    uint32_t v = 0xFFFFFFFFu;
+    if (lane < 8) v = __hip_atomic_load(q.heads + lane * q.stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t m = __ballot(lane < 8 && v < (q.items + 7u - (uint32_t)lane) / 8u) & 0xFFull;
+    if (m == 0) return 0xFFFFFFFFu;
+    const uint32_t rot = (uint32_t)(((m >> (xcc + 1)) | (m << (7 - xcc))) & 0xFFull);
+    s.h = (xcc + 1 + (uint32_t)__builtin_ctz(rot)) & 7u;
+    s.k = q_claim(q.heads + s.h * q.stride);
+  }
+}
+
+struct OctP {
+  using Ray = OctRay;
+  static constexpr int kFields = 2;
+  static constexpr int kMinWaves = RT_OCT_WAVES;
+  OctDev d;
+  template <bool FAST>
+  __device__ __forceinline__ int start(f3 o, f3 dir, f3 inv, float tf, Ray &R, float &t, f3 &n) const {
+    NoCnt c;
+    uint32_t node;
+    return oct_start<true, FAST>(d, o, dir, inv, 0.01f, tf, R, t, n, node, c);
+  }
+  template <bool FAST>
+  __device__ __forceinline__ int run(f3 o, f3 dir, f3 inv, float tf, LdsStack<kBlock, 2> st, Ray &R, int limit,
+                                     float &t, f3 &n) const {
+    NoCnt c;
+    uint32_t node;
+    return oct_run<kBlock, true, FAST, true>(d, o, dir, inv, 0.01f, tf, st, R, limit, t, n, node, c);
+  }
+};
+
+#ifndef RT_REFILL_MIN
+#define RT_REFILL_MIN 16  // dead lanes that trigger a refill (RTAMD_REFILL overrides)
+#endif
+
+#ifndef RT_PUMP_WAVES
+#define RT_PUMP_WAVES 0  // occupancy floor of the pump kernel: 0 = the scene's kMinWaves, 1 = the compiler's
+#endif
+template <class P, int SLOTS>
+__global__ __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(SLOTS > 7 ? 1 : (RT_PUMP_WAVES ? RT_PUMP_WAVES : P::kMinWaves))))
+void render_pump_kernel(P sc, FrameBatch fb, PersistQ q, int32_t nframes, int32_t refill_min) {
+  __shared__ uint32_t stk[SLOTS * P::kFields * kBlock];
+  __shared__ PumpFrame frames[kMaxBatch];
+  if ((int)threadIdx.x < nframes) {
+    const FrameArgs &fa = fb.f[threadIdx.x];
+    PumpFrame &pf = frames[threadIdx.x];
+    for (int i = 0; i < 3; ++i) pf.o[i] = fa.P.camera_pos[i];
+    for (int i = 0; i < 16; ++i) {
+      pf.proj_inv[i] = fa.P.proj_inv[i];
+      pf.view_inv[i] = fa.P.view_inv[i];
+    }
+    pf.color = fa.color;
+    pf.t = fa.t;
+  }
+  __syncthreads();
+  const FrameArgs &F = fb.f[0];  // size, flags and tile are the same for every frame of a batch
+  const int lane = threadIdx.x & 63;
+  const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID
+  const bool clear = (F.flags & RT_FLAG_CLEAR) != 0, hits_only = (F.flags & RT_FLAG_HITS_ONLY) != 0;
+  const bool peer = (F.flags & RT_FLAG_TILE_NATURAL) != 0;
+  const uint32_t isz = 64u * q.gx * q.gy;  // pixels per item
+  ItemStream is{xcc, q_claim(q.heads + xcc * q.stride)};
+  uint32_t cur = take_item(q, is, xcc, lane), off = 0;
+  LdsStack<kBlock, P::kFields> st{stk + threadIdx.x};
+  typename P::Ray R;
+  bool live = false, fast = true;
+  uint32_t f = 0;
+  size_t idx = 0;
+  f3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f}, inv{kInf, kInf, 1.0f};
+  float tfar = 100.0f;
+  // Renderer::draw's store (raytracing.cpp:91-94) of a finished ray, Normal shading
+  auto finish = [&](int status, float t, f3 n) {
+    const bool hit = status == RAY_HIT;
+    const bool store = hit && !__builtin_isinf(t);
+    if (dot(n, d) > 0) n = n * -1.0f;
+    const f4 c{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
+    uint32_t *cp = frames[f].color + idx;
+    float *tp = frames[f].t + idx;
+    if (clear && !hits_only) {
+      fb_store(cp, store ? pack_rgba(c) : 0u, peer);
+      fb_store(tp, store ? t : kInf, peer);
+    } else if (store) {
+      fb_store(cp, pack_rgba(c), peer);
+      fb_store(tp, t, peer);
+    }
+  };
+  for (;;) {
+    // refill: every dead lane takes the next pixel of the wave's stream
+    while (cur != 0xFFFFFFFFu) {
+      const uint64_t dead = __ballot(!live);
+      const uint32_t ndead = (uint32_t)__popcll(dead);
+      if ((int)ndead < refill_min) break;
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dead >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
+      const uint32_t nxt = (off + ndead >= isz) ? take_item(q, is, xcc, lane) : 0xFFFFFFFFu;
+      // (frame, tile row, tile column) of the two items, wave-uniform (scalar divisions)
+      const uint32_t fc = cur / q.per_frame, rc = cur - fc * q.per_frame;
+      const uint32_t tyc = rc / q.tiles_x, txc = rc - tyc * q.tiles_x;
+      uint32_t fn = 0, txn = 0, tyn = 0;
+      if (nxt != 0xFFFFFFFFu) {
+        fn = nxt / q.per_frame;
+        const uint32_t rn = nxt - fn * q.per_frame;
+        tyn = rn / q.tiles_x;
+        txn = rn - tyn * q.tiles_x;
+      }
+      bool got = false;
+      uint32_t p = 0, tx = 0, ty = 0;
+      if (!live) {
+        if (off + rank < isz) { got = true; p = off + rank; f = fc; tx = txc; ty = tyc; }
+        else if (nxt != 0xFFFFFFFFu) { got = true; p = off + rank - isz; f = fn; tx = txn; ty = tyn; }
+      }
+      off += ndead;
+      if (off >= isz) { cur = nxt; off -= isz; }
+      if (got) {
+        const uint32_t tile = p >> 6;
+        const uint32_t ti = q.gx == 1 ? 0u : (tile & 1u), tj = q.gx == 1 ? tile : (tile >> 1);
+        const int x = (int)((tx * q.gx + ti) * 8 + (p & 7u));
+        const int yl = (int)((ty * q.gy + tj) * 8 + ((p >> 3) & 7u));
+        if (x < F.W && yl < F.rows_local) {
+          const int yo = image_row(yl, F);
+          const PumpFrame &pf = frames[f];
+          idx = (size_t)(peer ? yo : yl) * F.W + x;
+          o = f3{pf.o[0], pf.o[1], pf.o[2]};
+          d = eye_ray(x, F.H - yo - 1, F.W, F.H, pf.proj_inv, pf.view_inv);
+          inv = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+          fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+          tfar = clear ? 100.0f : std_min(100.0f, pf.t[idx]);  // std::min(tFar, tPrev)
+          float t = kInf;
+          f3 n{0.0f, 1.0f, 0.0f};
+          const int s = fast ? sc.template start<true>(o, d, inv, tfar, R, t, n)
+                             : sc.template start<false>(o, d, inv, tfar, R, t, n);
+          if (s == RAY_PENDING) live = true;
+          else finish(s, t, n);
+        }
+      }
+    }
+    if (__ballot(live) == 0) {
+      if (cur == 0xFFFFFFFFu) break;
+      continue;
+    }
+    const int limit = cur == 0xFFFFFFFFu ? 0 : 64 - refill_min;
+    float t = kInf;
+    f3 n{0.0f, 1.0f, 0.0f};
+    int s = RAY_PENDING;
+    if (__ballot(live && !fast) == 0) {  // every live ray has finite 1/d: the fast slab form for all
+      if (live) s = sc.template run<true>(o, d, inv, tfar, st, R, limit, t, n);
+    } else {  // the exact ISPC form (the same bits for finite 1/d too)
+      if (live) s = sc.template run<false>(o, d, inv, tfar, st, R, limit, t, n);
+    }
+    if (live && s != RAY_PENDING) {
+      finish(s, t, n);
+      live = false;
+    }
+  }
+  if (lane == 0) {
+    uint32_t *done = q.heads + 8 * q.stride;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
       for (int i = 0; i < 8; ++i)
         __hip_atomic_store(q.heads + i * q.stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -688,6 +928,14 @@ struct rt_scene {
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
+  // cost-ordered work queue of the multi-frame launches, one per stream (queue_order)
+  struct QSched {
+    uint32_t *cost = nullptr, *order = nullptr;
+    uint32_t cap = 0, key = 0;
+  };
+  std::map<hipStream_t, QSched> qsched;
+  bool qorder_on = true;
+  bool pump_on = false;  // primary-ray batches on the ray pump (rtx_set_pump)
 };
 
 namespace {
@@ -915,6 +1163,10 @@ int stream_queue(hipStream_t stream, uint32_t **out) {
   return RT_OK;
 }
 
+// diagnostic per-wave stamps of the persistent launches (rtx_set_persist_stamps)
+unsigned long long *g_persist_stamps = nullptr;
+int64_t g_persist_stamps_cap = 0;
+
 // RTAMD_PERSIST=0 selects the one-block-per-16x16-tile dispatch (A/B switch).
 bool persist_enabled() {
   static const bool on = [] {
@@ -934,24 +1186,29 @@ int persist_group(int dflt) {
   return (g == 1 || g == 2 || g == 4) ? g : dflt;
 }
 
-template <class S, int MAXD, bool GENERAL>
-int launch_persist_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, int group,
-                     hipStream_t stream) {
-  static int blocks = 0;
-  static int dev_cached = -1;
+// Resident workgroups of a persistent kernel on the current device (cached per
+// kernel instantiation and device).
+template <class K>
+int resident_blocks(K kernel, int &blocks, int &dev_cached) {
   int dev = 0;
-  (void)hipGetDevice(&dev);
+  HIP_TRY(hipGetDevice(&dev));
   if (blocks == 0 || dev != dev_cached) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_persist_kernel<S, MAXD, GENERAL>,
-                                                         kBlock, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     blocks = std::max(1, per_cu) * std::max(1, cus);
     dev_cached = dev;
   }
+  return RT_OK;
+}
+
+// Work queue of one multi-frame launch: items of `group` 8x8 wave tiles
+// (1: 1x1, 2: 2x1, 4: 2x2) of n frames, the stream's head set; *grid = the
+// launch's workgroups (the resident ones, fewer for a small batch).
+int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t stream, PersistQ &q,
+               uint32_t &grid) {
   uint32_t *heads = nullptr;
   if (const int rc = stream_queue(stream, &heads)) return rc;
-  PersistQ q;
   q.heads = heads;
   static const uint32_t stride = [] {
     const char *e = std::getenv("RTAMD_QSTRIDE");
@@ -964,14 +1221,124 @@ int launch_persist_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int 
   q.tiles_x = (uint32_t)((fb.f[0].W + 8 * q.gx - 1) / (8 * q.gx));
   q.per_frame = q.tiles_x * (uint32_t)((fb.f[0].rows_local + 8 * q.gy - 1) / (8 * q.gy));
   q.items = q.per_frame * (uint32_t)n;
-  const uint32_t grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
+  grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
   q.waves = grid * (kBlock / 64);
+  q.stamps = (g_persist_stamps && (int64_t)q.waves <= g_persist_stamps_cap) ? g_persist_stamps : nullptr;
+  q.order = nullptr;
+  q.cost = nullptr;
+  q.nframes = (uint32_t)n;
+  q.interleave = 0;
+  return RT_OK;
+}
+
+// Item order of the multi-frame launches (RTAMD_QORDER, A/B switch): 0 =
+// frame-major natural order (default), 1 = cost-ordered (queue_order), 2 =
+// frames interleaved in natural tile order. rtx_set_qorder(scene, 0) forces 0.
+int qorder_mode() {
+  static const int m = [] {
+    const char *e = std::getenv("RTAMD_QORDER");
+    return e ? std::atoi(e) : 0;
+  }();
+  return m;
+}
+
+// Cost-ordered queue of a launch on `stream`: the stream's cost array (tile
+// costs of the previous launch on this stream; a new tile layout starts from
+// zeros) is turned into this launch's tile order by order_kernel (descending
+// cost class, which also clears the costs for this launch to collect). Each
+// stream has its own pair, so no launch reads what a concurrent one writes.
+// Stream-ordered: no host synchronisation.
+int queue_order(rt_scene *s, hipStream_t stream, PersistQ &q, int n) {
+  q.order = nullptr;
+  q.cost = nullptr;
+  q.nframes = (uint32_t)n;
+  q.interleave = 0;
+  if (!s || !s->qorder_on || qorder_mode() == 0) return RT_OK;
+  if (qorder_mode() == 2) {
+    q.interleave = 1;
+    return RT_OK;
+  }
+  rt_scene::QSched &qs = s->qsched[stream];
+  const uint32_t key = q.per_frame ^ (q.tiles_x << 20) ^ (q.gx << 30) ^ (q.gy << 31);
+  if (q.per_frame > qs.cap) {
+    if (qs.cost) (void)hipFreeAsync(qs.cost, stream);
+    if (qs.order) (void)hipFreeAsync(qs.order, stream);
+    qs.cost = qs.order = nullptr;
+    qs.cap = 0;
+    HIP_TRY(hipMallocAsync((void **)&qs.cost, (size_t)q.per_frame * 4, stream));
+    HIP_TRY(hipMallocAsync((void **)&qs.order, (size_t)q.per_frame * 4, stream));
+    qs.cap = q.per_frame;
+    qs.key = ~key;
+  }
+  if (qs.key != key) {
+    HIP_TRY(hipMemsetAsync(qs.cost, 0, (size_t)q.per_frame * 4, stream));
+    qs.key = key;
+  }
+  order_kernel<<<1, 1024, 0, stream>>>(qs.cost, qs.order, q.per_frame);
+  HIP_TRY(hipGetLastError());
+  q.order = qs.order;
+  q.cost = qs.cost;
+  return RT_OK;
+}
+
+template <class S, int MAXD, bool GENERAL>
+int launch_persist_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, int group,
+                     hipStream_t stream) {
+  static int blocks = 0, dev_cached = -1;
+  if (const int rc = resident_blocks(render_persist_kernel<S, MAXD, GENERAL>, blocks, dev_cached)) return rc;
+  PersistQ q;
+  uint32_t grid = 0;
+  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid)) return rc;
+  if (const int rc = queue_order(s, stream, q, n)) return rc;
   render_persist_kernel<S, MAXD, GENERAL><<<grid, kBlock, 0, stream>>>(sc, pl, fb, q);
   return RT_OK;
 }
 
+// The ray pump is measured slower than one tile per wave on every scene (DESIGN.md
+// section 8: refills break the coherence of a wave's rays), so primary-ray batches
+// take render_persist_kernel unless RTAMD_PUMP=1 or rtx_set_pump(scene, 1) asks
+// for the pump; RTAMD_REFILL=<lanes> sets its refill threshold.
+bool pump_env() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_PUMP");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+int refill_min() {
+  static const int v = [] {
+    const char *e = std::getenv("RTAMD_REFILL");
+    const int r = e ? std::atoi(e) : 0;
+    return (r >= 1 && r <= 64) ? r : RT_REFILL_MIN;
+  }();
+  return v;
+}
+
+// scenes with a ray-pump adapter (primary-ray batches)
+template <class S>
+struct PumpOf {
+  static constexpr bool kHas = false;
+};
+template <>
+struct PumpOf<OctS> {
+  static constexpr bool kHas = true;
+  using P = OctP;
+  static P make(const OctS &s) { return P{s.d}; }
+};
+
+template <class P, int MAXD>
+int launch_pump_t(const P &sc, const FrameBatch &fb, int n, int group, hipStream_t stream) {
+  static int blocks = 0, dev_cached = -1;
+  if (const int rc = resident_blocks(render_pump_kernel<P, MAXD>, blocks, dev_cached)) return rc;
+  PersistQ q;
+  uint32_t grid = 0;
+  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid)) return rc;
+  render_pump_kernel<P, MAXD><<<grid, kBlock, 0, stream>>>(sc, fb, q, n, refill_min());
+  return RT_OK;
+}
+
 template <class S, int MAXD>
-int launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
+int launch_batch_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
                    hipStream_t stream) {
   // Row-band tiles (a rank's share of a multi-GPU frame) take the block
   // dispatch: with 1/N of the pixels per launch the queue's drain (a wave
@@ -980,8 +1347,12 @@ int launch_batch_t(const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n,
   // ms/frame; of 8: 0.037 vs 0.021; at N = 2 the two are level).
   const int group = persist_group(S::kQueueGroup);
   if (persist_enabled() && group > 0 && fb.f[0].nranks <= 1) {
-    return general ? launch_persist_t<S, MAXD, true>(sc, pl, fb, n, group, stream)
-                   : launch_persist_t<S, MAXD, false>(sc, pl, fb, n, group, stream);
+    if constexpr (PumpOf<S>::kHas) {
+      if (!general && (pump_env() || (s && s->pump_on)))
+        return launch_pump_t<typename PumpOf<S>::P, MAXD>(PumpOf<S>::make(sc), fb, n, group, stream);
+    }
+    return general ? launch_persist_t<S, MAXD, true>(s, sc, pl, fb, n, group, stream)
+                   : launch_persist_t<S, MAXD, false>(s, sc, pl, fb, n, group, stream);
   }
   const dim3 grid((fb.f[0].W + kTile - 1) / kTile, (fb.f[0].rows_local + kTile - 1) / kTile, n);
   if (general)
@@ -1004,27 +1375,27 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
   if (s->kind == RT_SCENE_MESH) {
     MeshS sc{mesh_dev(s)};
     switch (s->maxd) {
-      case 4: rc = launch_batch_t<MeshS, 4>(sc, s->plane, fb, n, general, stream); break;
-      case 7: rc = launch_batch_t<MeshS, 7>(sc, s->plane, fb, n, general, stream); break;
-      case 15: rc = launch_batch_t<MeshS, 15>(sc, s->plane, fb, n, general, stream); break;
-      default: rc = launch_batch_t<MeshS, 31>(sc, s->plane, fb, n, general, stream); break;
+      case 4: rc = launch_batch_t<MeshS, 4>(s, sc, s->plane, fb, n, general, stream); break;
+      case 7: rc = launch_batch_t<MeshS, 7>(s, sc, s->plane, fb, n, general, stream); break;
+      case 15: rc = launch_batch_t<MeshS, 15>(s, sc, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<MeshS, 31>(s, sc, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_GRID) {
     const GridDev gd = grid_dev(s);
     switch (grid_mode(s, gd)) {
       case kGridBuf | kGridBricked:
-        rc = launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream);
+        rc = launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>(s, {gd}, s->plane, fb, n, general, stream);
         break;
-      case kGridBricked: rc = launch_batch_t<GridS<kGridBricked>, 1>({gd}, s->plane, fb, n, general, stream); break;
-      default: rc = launch_batch_t<GridS<kGridBuf>, 1>({gd}, s->plane, fb, n, general, stream); break;
+      case kGridBricked: rc = launch_batch_t<GridS<kGridBricked>, 1>(s, {gd}, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<GridS<kGridBuf>, 1>(s, {gd}, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_OCTREE) {
     OctS sc{OctDev{s->d_child, s->d_ovals}};
     switch (s->maxd) {
-      case 4: rc = launch_batch_t<OctS, 4>(sc, s->plane, fb, n, general, stream); break;
-      case 7: rc = launch_batch_t<OctS, 7>(sc, s->plane, fb, n, general, stream); break;
-      case 15: rc = launch_batch_t<OctS, 15>(sc, s->plane, fb, n, general, stream); break;
-      default: rc = launch_batch_t<OctS, 31>(sc, s->plane, fb, n, general, stream); break;
+      case 4: rc = launch_batch_t<OctS, 4>(s, sc, s->plane, fb, n, general, stream); break;
+      case 7: rc = launch_batch_t<OctS, 7>(s, sc, s->plane, fb, n, general, stream); break;
+      case 15: rc = launch_batch_t<OctS, 15>(s, sc, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<OctS, 31>(s, sc, s->plane, fb, n, general, stream); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
@@ -1335,6 +1706,10 @@ int rt_scene_destroy(rt_scene *s) {
                   s->d_cost, s->d_order};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  for (auto &kv : s->qsched) {
+    if (kv.second.cost) (void)hipFree(kv.second.cost);
+    if (kv.second.order) (void)hipFree(kv.second.order);
+  }
   if (s->sched_ev) (void)hipEventDestroy(s->sched_ev);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -1701,10 +2076,34 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
   return RT_OK;
 }
 
+// Diagnostic: persistent launches from now on write per-wave stamps (see
+// PersistQ::stamps) into the device buffer d_buf of cap_waves x 4 u64
+// (d_buf = NULL turns it off). Not part of include/rtamd.h.
+int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
+  g_persist_stamps = (unsigned long long *)d_buf;
+  g_persist_stamps_cap = d_buf ? cap_waves : 0;
+  return RT_OK;
+}
+
 // Diagnostic A/B switch: cooperative tail of the mesh primary path on (default) / off.
 int rtx_set_coop(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   s->coop = on != 0;
+  return RT_OK;
+}
+
+// Diagnostic switch: primary-ray batches of this scene on the ray pump
+// (render_pump_kernel) instead of one tile per wave (default off).
+int rtx_set_pump(rt_scene *s, int on) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  s->pump_on = on != 0;
+  return RT_OK;
+}
+
+// Diagnostic A/B switch: cost-ordered work queue of the multi-frame launches on (default) / off.
+int rtx_set_qorder(rt_scene *s, int on) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  s->qorder_on = on != 0;
   return RT_OK;
 }
 

@@ -1022,34 +1022,63 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
   }
 }
 
-template <int BLOCK, bool NEED_NORMAL, bool FAST, class CT>
-__device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear,
-                                            float tFar, LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
-                                            uint32_t &out_node, CT &cnt) {
+// Traversal state of one octree ray below the root expansion: the top frame
+// (the children block (childrenOffset) of the node whose children are being
+// visited, its remaining list and its coordinates) lives here, the frames
+// below it in LDS slots [0, depth-1]. Frames keep the block, not the node, so
+// visiting a child costs one dependent load (its word), not two. The state is
+// resumable: oct_run can suspend a ray between two iterations and continue it
+// later in the same lane (the ray pump, render_pump_kernel).
+struct OctRay {
+  uint32_t fbase;
+  uint32_t lc;  // remaining child ids (3 bits each, next in the low bits) | count << 24
+  uint32_t ix, iy, iz;
+  int32_t depth;  // depth of the top frame's node (root = 0)
+};
+// ray status: still traversing (suspended), finished without a hit, with a hit
+enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
+
+// SDFOctree::intersect -> intersectNode(0) (octree_raytracing.cpp:166-208), root stage.
+template <bool NEED_NORMAL, bool FAST, class CT>
+__device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
+                                         OctRay &R, float &out_t, f3 &out_n, uint32_t &out_node, CT &cnt) {
   const uint32_t root = sc.child[0];
   cnt.add(C_OCT_NODE, 1);
   if (root == 0 || root == rtl::kOctNeverHits) {
     cnt.add(C_OCT_LEAF, 1);
-    if (root == rtl::kOctNeverHits) return false;
+    if (root == rtl::kOctNeverHits) return RAY_MISS;
     out_node = 0;
-    return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d,
-                                 inv, tNear, tFar, out_t, out_n, cnt);
+    return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv,
+                                 tNear, tFar, out_t, out_n, cnt)
+               ? RAY_HIT
+               : RAY_MISS;
   }
-  // top frame: the children block (childrenOffset) of the node whose children
-  // are being visited, its coords and list; frames keep the block, not the
-  // node, so visiting a child costs one dependent load (its word), not two
-  uint32_t fbase = root, flist, fcnt;
-  uint32_t ix = 0, iy = 0, iz = 0;
-  int depth = 0;  // depth of fnode (root = 0); frames below the top live in LDS
-  {
-    f3 bmin, bmax;
-    float inv_s;
-    oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
-    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, flist, fcnt);
-  }
+  f3 bmin, bmax;
+  float inv_s;
+  oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
+  uint32_t l, c;
+  oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
+  R = OctRay{root, l | (c << 24), 0u, 0u, 0u, 0};
+  return c == 0 ? RAY_MISS : RAY_PENDING;
+}
+
+// The front-to-back loop of intersectNode below the root. SUSPEND: before each
+// iteration, if `limit` or fewer lanes of the wave are still in the loop, save
+// the state and return RAY_PENDING.
+template <int BLOCK, bool NEED_NORMAL, bool FAST, bool SUSPEND, class CT>
+__device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
+                                       LdsStack<BLOCK, 2> st, OctRay &R, int limit, float &out_t, f3 &out_n,
+                                       uint32_t &out_node, CT &cnt) {
+  uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24;
+  uint32_t ix = R.ix, iy = R.iy, iz = R.iz;
+  int depth = R.depth;
   for (;;) {
+    if (SUSPEND && __popcll(__ballot(1)) <= limit) {
+      R = OctRay{fbase, flist | (fcnt << 24), ix, iy, iz, depth};
+      return RAY_PENDING;
+    }
     if (fcnt == 0) {
-      if (depth == 0) return false;
+      if (depth == 0) return RAY_MISS;
       --depth;
       fbase = st.at(depth, 0);
       const uint32_t lc = st.at(depth, 1);
@@ -1074,7 +1103,7 @@ __device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv
       if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, out_n,
                                 cnt)) {
         out_node = cn;
-        return true;
+        return RAY_HIT;
       }
       continue;
     }
@@ -1087,6 +1116,17 @@ __device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv
     fbase = cw; flist = l; fcnt = c;
     ix = cx; iy = cy; iz = cz;
   }
+}
+
+template <int BLOCK, bool NEED_NORMAL, bool FAST, class CT>
+__device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear,
+                                            float tFar, LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
+                                            uint32_t &out_node, CT &cnt) {
+  OctRay R;
+  const int s = oct_start<NEED_NORMAL, FAST>(sc, o, d, inv, tNear, tFar, R, out_t, out_n, out_node, cnt);
+  if (s != RAY_PENDING) return s == RAY_HIT;
+  return oct_run<BLOCK, NEED_NORMAL, FAST, false>(sc, o, d, inv, tNear, tFar, st, R, 0, out_t, out_n, out_node,
+                                                  cnt) == RAY_HIT;
 }
 
 template <int BLOCK, bool NEED_NORMAL, class CT>
