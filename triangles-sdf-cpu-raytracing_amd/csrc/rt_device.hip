@@ -122,7 +122,7 @@ struct GridS {
   }
 };
 struct OctS {
-  static constexpr int kFields = 2;
+  static constexpr int kFields = kOctFields;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   static constexpr int kQueueGroup = 2;
@@ -622,7 +622,7 @@ __device__ __forceinline__ uint32_t take_item(const PersistQ &q, ItemStream &s, 
 
 struct OctP {
   using Ray = OctRay;
-  static constexpr int kFields = 2;
+  static constexpr int kFields = kOctFields;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   OctDev d;
   template <bool FAST>
@@ -632,7 +632,7 @@ struct OctP {
     return oct_start<true, FAST>(d, o, dir, inv, 0.01f, tf, R, t, n, node, c);
   }
   template <bool FAST>
-  __device__ __forceinline__ int run(f3 o, f3 dir, f3 inv, float tf, LdsStack<kBlock, 2> st, Ray &R, int limit,
+  __device__ __forceinline__ int run(f3 o, f3 dir, f3 inv, float tf, LdsStack<kBlock, kOctFields> st, Ray &R, int limit,
                                      float &t, f3 &n) const {
     NoCnt c;
     uint32_t node;
@@ -906,7 +906,7 @@ struct rt_scene {
   uint32_t size[3] = {0, 0, 0};
   bool grid_bricked = false;  // device layout (rt_scenes.h GridDev): bricked, or the reference's linear
   // octree
-  uint32_t *d_child = nullptr;
+  rtl::OctWord *d_child = nullptr;
   rtl::OctVals *d_ovals = nullptr;
   int32_t oct_depth = 0;
   PlaneDev plane{};

@@ -636,10 +636,10 @@ bool flatten_octree(const uint8_t *nodes36, int64_t count, OctGpu &out, std::str
         all0 = all0 && (v[k] == 0.0f);
         allAbove = allAbove && (v[k] >= 1e-4f);
       }
-      out.child[(size_t)i] = (all10 || all0 || allAbove) ? rtl::kOctNeverHits : 0u;
+      out.child[(size_t)i] = rtl::OctWord{(all10 || all0 || allAbove) ? rtl::kOctNeverHits : 0u, 0u};
     } else {
       if ((int64_t)off + 7 >= count || off == rtl::kOctNeverHits) { err = "octree child offset out of range"; return false; }
-      out.child[(size_t)i] = off;
+      out.child[(size_t)i] = rtl::OctWord{off, 0u};
     }
   }
   // depth (levels of inner nodes on the deepest path), with a cycle guard
@@ -649,11 +649,39 @@ bool flatten_octree(const uint8_t *nodes36, int64_t count, OctGpu &out, std::str
     auto [n, d] = st.back();
     st.pop_back();
     if (++visited > count || d > 24) { err = "octree is cyclic or deeper than 24 levels"; return false; }
-    const uint32_t c = out.child[n];
+    const uint32_t c = out.child[n].child;
     if (c != 0 && c != rtl::kOctNeverHits) {
       out.max_depth = std::max(out.max_depth, d + 1);
       for (int k = 0; k < 8; ++k) st.push_back({c + (uint32_t)k, d + 1});
     }
+  }
+  // child masks (rtl::OctWord), bottom-up: can_hit(node) = a leaf that can hit,
+  // or an inner node with a child that can hit. Post-order over the (acyclic,
+  // checked above) node graph; nodes reachable along several paths are computed once.
+  std::vector<int8_t> can((size_t)count, -1);
+  std::vector<std::pair<uint32_t, bool>> post{{0u, false}};
+  while (!post.empty()) {
+    auto [n, expanded] = post.back();
+    post.pop_back();
+    if (can[n] >= 0) continue;
+    const uint32_t c = out.child[n].child;
+    if (c == 0 || c == rtl::kOctNeverHits) {
+      can[n] = c == 0 ? 1 : 0;
+      continue;
+    }
+    if (!expanded) {
+      post.push_back({n, true});
+      for (int k = 0; k < 8; ++k)
+        if (can[c + k] < 0) post.push_back({c + (uint32_t)k, false});
+      continue;
+    }
+    uint32_t m = 0;
+    for (int k = 0; k < 8; ++k) {
+      if (can[c + k] > 0) m |= 1u << k;
+      if (out.child[c + k].child == 0) m |= 1u << (8 + k);
+    }
+    out.child[n].masks = m;
+    can[n] = (m & 0xFFu) ? 1 : 0;
   }
   return true;
 }

@@ -37,7 +37,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
                 std::string &err);
 
 struct OctGpu {
-  std::vector<uint32_t> child;        // per node: 0 leaf, kOctNeverHits, or childrenOffset
+  std::vector<rtl::OctWord> child;    // per node: {0 leaf, kOctNeverHits or childrenOffset; child masks}
   std::vector<rtl::OctVals> vals;     // per node corner values
   int32_t max_depth = 0;
 };

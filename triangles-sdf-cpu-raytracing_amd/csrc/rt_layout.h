@@ -52,6 +52,18 @@ static_assert(sizeof(GTri) == 48, "GTri must be 48 bytes");
 // >= HIT_EPS, octree_raytracing.cpp:125-133); otherwise childrenOffset.
 constexpr uint32_t kOctNeverHits = 0xFFFFFFFFu;
 
+// Device word of an octree node: `child` as above, and for an inner node the
+// masks of its 8 children (bit k = child id k, (x<<2)|(y<<1)|z):
+//   bits 0-7  the child's subtree can produce a hit (a leaf that can hit, or an
+//             inner node with such a leaf below it); the reference's recursion
+//             into any other child returns false whatever the ray
+//             (octree_raytracing.cpp:122-133, 166-202), so the traversal may skip it;
+//   bits 8-15 the child is a leaf that can hit (march it without loading its word).
+struct alignas(8) OctWord {
+  uint32_t child;
+  uint32_t masks;
+};
+
 struct alignas(32) OctVals {
   float v[8];
 };

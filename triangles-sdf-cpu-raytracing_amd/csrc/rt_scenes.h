@@ -19,9 +19,11 @@ namespace rtd {
 enum { C_BVH_INNER = 0, C_BVH_LEAF, C_BVH_TRI, C_GRID_SDF, C_OCT_NODE, C_OCT_LEAF, C_OCT_STEP,
        C_OCT_NORMAL, C_RAYS, C_NUM };
 struct NoCnt {
+  static constexpr bool kCounts = false;
   __device__ __forceinline__ void add(int, uint32_t) {}
 };
 struct LaneCnt {
+  static constexpr bool kCounts = true;
   uint32_t v[C_NUM];
   __device__ __forceinline__ void add(int i, uint32_t n) { v[i] += n; }
 };
@@ -882,9 +884,10 @@ __device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, floa
 // integer coordinates i equals [-1 + i*s, -1 + i*s + s], s = 2^(1-k).
 // (tests/test_host.py checks this against the float chain for every node.)
 struct OctDev {
-  const uint32_t *__restrict__ child;
+  const rtl::OctWord *__restrict__ node;  // child word + child masks (rt_layout.h)
   const rtl::OctVals *__restrict__ vals;
 };
+constexpr int kOctFields = 3;  // LDS words per octree frame: children block, list | count, leaf mask
 
 __device__ __forceinline__ void oct_box(uint32_t ix, uint32_t iy, uint32_t iz, int depth, f3 &bmin,
                                         f3 &bmax, float &inv_s) {
@@ -1024,25 +1027,54 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
 
 // Traversal state of one octree ray below the root expansion: the top frame
 // (the children block (childrenOffset) of the node whose children are being
-// visited, its remaining list and its coordinates) lives here, the frames
-// below it in LDS slots [0, depth-1]. Frames keep the block, not the node, so
-// visiting a child costs one dependent load (its word), not two. The state is
+// visited, its remaining list, the leaf mask of that block and its
+// coordinates) lives here, the frames below it in LDS slots [0, depth-1].
+// Frames keep the block, not the node, so visiting a child costs one dependent
+// load (its word, or a leaf's corner values), not two. The state is
 // resumable: oct_run can suspend a ray between two iterations and continue it
 // later in the same lane (the ray pump, render_pump_kernel).
+//
+// Child masks (rtl::OctWord, the timed kernels; the counting variant, CT =
+// LaneCnt, walks every child as the reference does, so its work units are the
+// reference's): an inner node's sorted child list keeps only children whose
+// subtree can produce a hit -- a skipped child is a leaf intersectLeaf rejects
+// before marching (isEmpty() or every corner >= HIT_EPS,
+// octree_raytracing.cpp:125-133) or an inner node with only such leaves below
+// it, whose recursion returns false for every ray, so the first child that
+// hits is the same -- and a child flagged as a leaf that can hit is marched
+// straight away, without loading its word.
 struct OctRay {
   uint32_t fbase;
   uint32_t lc;  // remaining child ids (3 bits each, next in the low bits) | count << 24
+  uint32_t leafm;  // children of the top frame that are leaves that can hit (masked walk)
   uint32_t ix, iy, iz;
   int32_t depth;  // depth of the top frame's node (root = 0)
 };
 // ray status: still traversing (suspended), finished without a hit, with a hit
 enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 
+// the entries of a sorted child list (oct_expand) whose bit is set in keep
+__device__ __forceinline__ void oct_filter(uint32_t &list, uint32_t &cnt, uint32_t keep) {
+  uint32_t out = 0, n = 0, l = list;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t id = l & 7u;
+    if ((uint32_t)i < cnt && ((keep >> id) & 1u)) {
+      out |= id << (3 * n);
+      ++n;
+    }
+    l >>= 3;
+  }
+  list = out;
+  cnt = n;
+}
+
 // SDFOctree::intersect -> intersectNode(0) (octree_raytracing.cpp:166-208), root stage.
 template <bool NEED_NORMAL, bool FAST, class CT>
 __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                          OctRay &R, float &out_t, f3 &out_n, uint32_t &out_node, CT &cnt) {
-  const uint32_t root = sc.child[0];
+  const rtl::OctWord rw = sc.node[0];
+  const uint32_t root = rw.child;
   cnt.add(C_OCT_NODE, 1);
   if (root == 0 || root == rtl::kOctNeverHits) {
     cnt.add(C_OCT_LEAF, 1);
@@ -1058,7 +1090,8 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
   uint32_t l, c;
   oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
-  R = OctRay{root, l | (c << 24), 0u, 0u, 0u, 0};
+  if (!CT::kCounts) oct_filter(l, c, rw.masks);
+  R = OctRay{root, l | (c << 24), rw.masks >> 8, 0u, 0u, 0u, 0};
   return c == 0 ? RAY_MISS : RAY_PENDING;
 }
 
@@ -1067,14 +1100,15 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
 // the state and return RAY_PENDING.
 template <int BLOCK, bool NEED_NORMAL, bool FAST, bool SUSPEND, class CT>
 __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                       LdsStack<BLOCK, 2> st, OctRay &R, int limit, float &out_t, f3 &out_n,
-                                       uint32_t &out_node, CT &cnt) {
-  uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24;
+                                       LdsStack<BLOCK, kOctFields> st, OctRay &R, int limit, float &out_t,
+                                       f3 &out_n, uint32_t &out_node, CT &cnt) {
+  constexpr bool MASKS = !CT::kCounts;
+  uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24, leafm = R.leafm;
   uint32_t ix = R.ix, iy = R.iy, iz = R.iz;
   int depth = R.depth;
   for (;;) {
     if (SUSPEND && __popcll(__ballot(1)) <= limit) {
-      R = OctRay{fbase, flist | (fcnt << 24), ix, iy, iz, depth};
+      R = OctRay{fbase, flist | (fcnt << 24), leafm, ix, iy, iz, depth};
       return RAY_PENDING;
     }
     if (fcnt == 0) {
@@ -1082,6 +1116,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
       --depth;
       fbase = st.at(depth, 0);
       const uint32_t lc = st.at(depth, 1);
+      if (MASKS) leafm = st.at(depth, 2);
       flist = lc & 0xFFFFFFu;
       fcnt = lc >> 24;
       ix >>= 1; iy >>= 1; iz >>= 1;
@@ -1092,13 +1127,21 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     fcnt -= 1;
     const uint32_t cn = fbase + j;
     const uint32_t cx = (ix << 1) | (j >> 2), cy = (iy << 1) | ((j >> 1) & 1u), cz = (iz << 1) | (j & 1u);
-    const uint32_t cw = sc.child[cn];
-    cnt.add(C_OCT_NODE, 1);
-    if (cw == rtl::kOctNeverHits) { cnt.add(C_OCT_LEAF, 1); continue; }
+    rtl::OctWord cw{0u, 0u};
+    bool leaf;
+    if (MASKS) {
+      leaf = (leafm >> j) & 1u;  // a leaf that can hit: no word to load
+      if (!leaf) cw = sc.node[cn];
+    } else {
+      cw = sc.node[cn];
+      cnt.add(C_OCT_NODE, 1);
+      if (cw.child == rtl::kOctNeverHits) { cnt.add(C_OCT_LEAF, 1); continue; }
+      leaf = cw.child == 0;
+    }
     f3 bmin, bmax;
     float inv_s;
     oct_box(cx, cy, cz, depth + 1, bmin, bmax, inv_s);
-    if (cw == 0) {
+    if (leaf) {
       cnt.add(C_OCT_LEAF, 1);
       if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, out_n,
                                 cnt)) {
@@ -1109,18 +1152,21 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     }
     uint32_t l, c;
     oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
+    if (MASKS) oct_filter(l, c, cw.masks);
     if (c == 0) continue;
     st.at(depth, 0) = fbase;
     st.at(depth, 1) = flist | (fcnt << 24);
+    if (MASKS) st.at(depth, 2) = leafm;
     ++depth;
-    fbase = cw; flist = l; fcnt = c;
+    fbase = cw.child; flist = l; fcnt = c;
+    leafm = cw.masks >> 8;
     ix = cx; iy = cy; iz = cz;
   }
 }
 
 template <int BLOCK, bool NEED_NORMAL, bool FAST, class CT>
 __device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear,
-                                            float tFar, LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
+                                            float tFar, LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                             uint32_t &out_node, CT &cnt) {
   OctRay R;
   const int s = oct_start<NEED_NORMAL, FAST>(sc, o, d, inv, tNear, tFar, R, out_t, out_n, out_node, cnt);
@@ -1131,7 +1177,7 @@ __device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv
 
 template <int BLOCK, bool NEED_NORMAL, class CT>
 __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                          LdsStack<BLOCK, 2> st, float &out_t, f3 &out_n,
+                                          LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                           uint32_t &out_node, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z))
@@ -1141,7 +1187,7 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
 
 template <int BLOCK, class CT>
 __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK, 2> st, CT &cnt) {
+                                             LdsStack<BLOCK, kOctFields> st, CT &cnt) {
   Hit h = miss_hit();
   uint32_t node;
   if (oct_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, h.t, h.n, node, cnt)) {
@@ -1154,7 +1200,7 @@ __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float
 }
 template <int BLOCK, class CT>
 __device__ __forceinline__ bool oct_occluded(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
-                                             LdsStack<BLOCK, 2> st, CT &cnt) {
+                                             LdsStack<BLOCK, kOctFields> st, CT &cnt) {
   float t;
   f3 n;
   uint32_t node;
