@@ -146,42 +146,3 @@ def test_pump_refill_thresholds(gpu, refill):
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RTAMD_REFILL=refill, RTAMD_PUMP="1"),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
-
-
-def qorder_check(name):
-    """Launches alternating two streams and two frame sizes (a new tile layout
-    resets a stream's costs) equal one-frame renders."""
-    import ctypes as C
-
-    from rtamd import _lib
-    sc = S.gpu_scene(name)
-    sc.set_plane(None)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    for rep in range(6):
-        W, H = (256, 144) if rep % 3 != 2 else (97, 61)
-        prm = cams(W, H, 8 if rep % 2 else 5, seed=10 * rep)
-        bufs = [(torch.full((H, W), 7, dtype=torch.int32, device="cuda"),
-                 torch.zeros((H, W), dtype=torch.float32, device="cuda")) for _ in prm]
-        torch.cuda.synchronize()
-        st = streams[rep % 2]
-        sc.render_device_frames(prm, [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs],
-                                W, H, _lib.RT_FLAG_CLEAR, stream=st.cuda_stream)
-        torch.cuda.synchronize()
-        same(bufs, single(sc, prm, W, H), f"{name} launch {rep}")
-
-
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
-def test_queue_item_orders_are_output_neutral(gpu, mode):
-    """The work queue's item orders (RTAMD_QORDER: 0 frame-major, 1 cost-ordered
-    from the previous launch's per-stream tile costs, 2 frames interleaved) never
-    change a frame (child process: the mode is read once per process)."""
-    code = (
-        "import sys; sys.path[:0] = [%r, %r, %r]\n"
-        "import torch, test_pump as T\n"
-        "for name in ('stanford-bunny.obj', 'sdf_6.octree'):\n"
-        "    T.qorder_check(name)\n"
-        "print('ok')\n" % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
-                           os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd")))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RTAMD_QORDER=mode),
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -6,6 +6,9 @@ cost a and the per-frame cost b) and, from the per-wave stamps of one launch
 (rtx_set_persist_stamps): when the first wave found the queue drained, when the
 last wave ended (the tail between the two), and the spread of wave starts
 (the ramp).
+The stamps exist only in a diagnostic build of the library:
+  bash tools/build_variant.sh stamps -DRT_PERSIST_STAMPS
+  RTAMD_LIB=triangles-sdf-cpu-raytracing_amd/lib/var_stamps.so python tools/persist_tail.py bunny
 usage: python tools/persist_tail.py [workload ...]   (keys of bench.WORKLOADS)
 """
 import ctypes as C

@@ -476,19 +476,10 @@ struct PersistQ {
   uint32_t waves;    // waves in the grid
   uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
   uint32_t stride;   // words between heads
-  // diagnostic (rtx_set_persist_stamps; NULL in normal launches): per wave
-  // w = blockIdx.x * 4 + wave, 4 x u64 = start, end (s_memrealtime, 100 MHz),
-  // items traced, end of its last item
+  // diagnostic builds (-DRT_PERSIST_STAMPS, tools/build_variant.sh; see
+  // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 4 x u64 =
+  // start, end (s_memrealtime, 100 MHz), items traced, end of its last item
   unsigned long long *stamps;
-  // cost-ordered queue (queue_order; NULL = frame-major natural order): item i
-  // is tile order[i / nframes] of frame i % nframes, so the tiles that were
-  // slowest in the previous launch on this stream start first in every frame
-  // and the launch's tail is made of light tiles; cost[r] collects each tile's
-  // slowest item (shader cycles) of this launch for the next one.
-  const uint32_t *order;
-  uint32_t *cost;
-  uint32_t nframes;
-  uint32_t interleave;  // frames interleaved in natural tile order (no costs): item i = tile i / nframes of frame i % nframes
 };
 // 4 KiB + 256 B apart: every head on its own memory channel's lines, so the
 // memory-side atomics of different heads do not queue behind each other
@@ -508,9 +499,11 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
   const int lane = threadIdx.x & 63;
   const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
-  const unsigned long long t_start = q.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+#ifdef RT_PERSIST_STAMPS
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long t_item = t_start;
   uint32_t n_items = 0;
+#endif
   uint32_t h = xcc;
   uint32_t k = q_claim(q.heads + h * q.stride);
   NoCnt cnt{};
@@ -531,31 +524,19 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
       continue;
     }
     const uint32_t knext = q_claim(q.heads + h * q.stride);
-    uint32_t f, r;
-    if (q.order || q.interleave) {
-      const uint32_t rank = item / q.nframes;
-      f = item - rank * q.nframes;
-      r = q.order ? q.order[rank] : rank;
-    } else {
-      f = item / q.per_frame;
-      r = item - f * q.per_frame;
-    }
-    const uint64_t c0 = q.cost ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
     for (uint32_t j = 0; j < q.gy; ++j)
       for (uint32_t i = 0; i < q.gx; ++i)
         render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[f], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
                                             (int)((ty * q.gy + j) * 8) + (lane >> 3));
-    if (q.cost) {
-      const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
-      if (lane == 0) atomicMax(q.cost + r, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt);
-    }
-    if (q.stamps) {
-      ++n_items;
-      t_item = __builtin_amdgcn_s_memrealtime();
-    }
+#ifdef RT_PERSIST_STAMPS
+    ++n_items;
+    t_item = __builtin_amdgcn_s_memrealtime();
+#endif
     k = knext;
   }
+#ifdef RT_PERSIST_STAMPS
   if (q.stamps && lane == 0) {
     const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     q.stamps[4 * w] = t_start;
@@ -563,6 +544,7 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
     q.stamps[4 * w + 2] = n_items | ((unsigned long long)xcc << 32);
     q.stamps[4 * w + 3] = t_item;
   }
+#endif
   if (lane == 0) {
     uint32_t *done = q.heads + 8 * q.stride;
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
@@ -677,7 +659,7 @@ void render_pump_kernel(P sc, FrameBatch fb, PersistQ q, int32_t nframes, int32_
   typename P::Ray R;
   bool live = false, fast = true;
   uint32_t f = 0;
-  size_t idx = 0;
+  uint32_t idx = 0;
   f3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f}, inv{kInf, kInf, 1.0f};
   float tfar = 100.0f;
   // Renderer::draw's store (raytracing.cpp:91-94) of a finished ray, Normal shading
@@ -731,7 +713,7 @@ void render_pump_kernel(P sc, FrameBatch fb, PersistQ q, int32_t nframes, int32_
         if (x < F.W && yl < F.rows_local) {
           const int yo = image_row(yl, F);
           const PumpFrame &pf = frames[f];
-          idx = (size_t)(peer ? yo : yl) * F.W + x;
+          idx = (uint32_t)(peer ? yo : yl) * (uint32_t)F.W + (uint32_t)x;
           o = f3{pf.o[0], pf.o[1], pf.o[2]};
           d = eye_ray(x, F.H - yo - 1, F.W, F.H, pf.proj_inv, pf.view_inv);
           inv = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -928,13 +910,6 @@ struct rt_scene {
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
-  // cost-ordered work queue of the multi-frame launches, one per stream (queue_order)
-  struct QSched {
-    uint32_t *cost = nullptr, *order = nullptr;
-    uint32_t cap = 0, key = 0;
-  };
-  std::map<hipStream_t, QSched> qsched;
-  bool qorder_on = true;
   bool pump_on = false;  // primary-ray batches on the ray pump (rtx_set_pump)
 };
 
@@ -1224,60 +1199,6 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
   q.waves = grid * (kBlock / 64);
   q.stamps = (g_persist_stamps && (int64_t)q.waves <= g_persist_stamps_cap) ? g_persist_stamps : nullptr;
-  q.order = nullptr;
-  q.cost = nullptr;
-  q.nframes = (uint32_t)n;
-  q.interleave = 0;
-  return RT_OK;
-}
-
-// Item order of the multi-frame launches (RTAMD_QORDER, A/B switch): 0 =
-// frame-major natural order (default), 1 = cost-ordered (queue_order), 2 =
-// frames interleaved in natural tile order. rtx_set_qorder(scene, 0) forces 0.
-int qorder_mode() {
-  static const int m = [] {
-    const char *e = std::getenv("RTAMD_QORDER");
-    return e ? std::atoi(e) : 0;
-  }();
-  return m;
-}
-
-// Cost-ordered queue of a launch on `stream`: the stream's cost array (tile
-// costs of the previous launch on this stream; a new tile layout starts from
-// zeros) is turned into this launch's tile order by order_kernel (descending
-// cost class, which also clears the costs for this launch to collect). Each
-// stream has its own pair, so no launch reads what a concurrent one writes.
-// Stream-ordered: no host synchronisation.
-int queue_order(rt_scene *s, hipStream_t stream, PersistQ &q, int n) {
-  q.order = nullptr;
-  q.cost = nullptr;
-  q.nframes = (uint32_t)n;
-  q.interleave = 0;
-  if (!s || !s->qorder_on || qorder_mode() == 0) return RT_OK;
-  if (qorder_mode() == 2) {
-    q.interleave = 1;
-    return RT_OK;
-  }
-  rt_scene::QSched &qs = s->qsched[stream];
-  const uint32_t key = q.per_frame ^ (q.tiles_x << 20) ^ (q.gx << 30) ^ (q.gy << 31);
-  if (q.per_frame > qs.cap) {
-    if (qs.cost) (void)hipFreeAsync(qs.cost, stream);
-    if (qs.order) (void)hipFreeAsync(qs.order, stream);
-    qs.cost = qs.order = nullptr;
-    qs.cap = 0;
-    HIP_TRY(hipMallocAsync((void **)&qs.cost, (size_t)q.per_frame * 4, stream));
-    HIP_TRY(hipMallocAsync((void **)&qs.order, (size_t)q.per_frame * 4, stream));
-    qs.cap = q.per_frame;
-    qs.key = ~key;
-  }
-  if (qs.key != key) {
-    HIP_TRY(hipMemsetAsync(qs.cost, 0, (size_t)q.per_frame * 4, stream));
-    qs.key = key;
-  }
-  order_kernel<<<1, 1024, 0, stream>>>(qs.cost, qs.order, q.per_frame);
-  HIP_TRY(hipGetLastError());
-  q.order = qs.order;
-  q.cost = qs.cost;
   return RT_OK;
 }
 
@@ -1289,7 +1210,6 @@ int launch_persist_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBa
   PersistQ q;
   uint32_t grid = 0;
   if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid)) return rc;
-  if (const int rc = queue_order(s, stream, q, n)) return rc;
   render_persist_kernel<S, MAXD, GENERAL><<<grid, kBlock, 0, stream>>>(sc, pl, fb, q);
   return RT_OK;
 }
@@ -1706,10 +1626,6 @@ int rt_scene_destroy(rt_scene *s) {
                   s->d_cost, s->d_order};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  for (auto &kv : s->qsched) {
-    if (kv.second.cost) (void)hipFree(kv.second.cost);
-    if (kv.second.order) (void)hipFree(kv.second.order);
-  }
   if (s->sched_ev) (void)hipEventDestroy(s->sched_ev);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -2097,13 +2013,6 @@ int rtx_set_coop(rt_scene *s, int on) {
 int rtx_set_pump(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   s->pump_on = on != 0;
-  return RT_OK;
-}
-
-// Diagnostic A/B switch: cost-ordered work queue of the multi-frame launches on (default) / off.
-int rtx_set_qorder(rt_scene *s, int on) {
-  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
-  s->qorder_on = on != 0;
   return RT_OK;
 }
 
