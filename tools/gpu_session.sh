@@ -17,8 +17,10 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench) run bench 900 python bench.py --gpus 1 --steps 20 --warmup 5 && tail -1 "$OUT/bench.log" > "$OUT/bench.json" || exit 1 ;;
     bench128) run bench128 600 python bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline --no-extra && tail -1 "$OUT/bench128.log" > "$OUT/bench128.json" || exit 1 ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o p -- python3 bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline || exit 1 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o p -- python3 bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline || exit 1 ;;
     split) run split 600 python tools/ab.py split bunny || exit 1 ;;
+    dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && tail -1 "$OUT/dist_gloo.log" > "$OUT/dist_gloo.json" || exit 1 ;;
+    dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && tail -1 "$OUT/dist_rccl1.log" > "$OUT/dist_rccl1.json" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
