@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 4
+#define RTAMD_ABI_VERSION 5
 
 enum rt_status {
   RT_OK = 0,
@@ -119,6 +119,13 @@ int rt_camera(const float pos[3], const float target[3], const float up[3], floa
  * protocol on *nnodes. Used to check the tree against the reference's. */
 int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
                   uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth);
+/* Which builder rt_scene_create_mesh / rt_bvh_export use for BVHBuilder::perform
+ * (src/triangles_raytracing.cpp:12-258): RT_BVH_HOST (OpenMP on the host),
+ * RT_BVH_DEVICE (on the current HIP device: libstdc++'s introsort replicated
+ * with parallel partitions, SAH sweeps as device scans) or RT_BVH_AUTO (the
+ * device from 131,072 triangles). Both give the identical tree. Process-wide. */
+enum rt_bvh_builder { RT_BVH_AUTO = 0, RT_BVH_HOST = 1, RT_BVH_DEVICE = 2 };
+int rt_set_bvh_builder(int mode);
 
 /* ---- scenes ------------------------------------------------------------- */
 /* BVHBuilder::perform (src/triangles_raytracing.cpp:227-258): builds the same

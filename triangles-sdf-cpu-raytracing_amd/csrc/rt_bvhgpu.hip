@@ -1,0 +1,881 @@
+// rt_bvhgpu.hip -- BVHBuilder::perform (triangles_raytracing.cpp:12-258) on the
+// GPU: the SAME tree as the host build (rt_host.cpp build_bvh8), bit for bit.
+//
+// The tree depends on the order std::sort leaves triangles with equal keys
+// (their bbox max on the split axis; triangles sharing a vertex tie), so the
+// device sort replicates libstdc++'s introsort exactly instead of using a
+// radix or merge sort:
+//  * a segment longer than kSerialMax is partitioned by the whole grid: the
+//    median of three moves to the front (std::__move_median_to_first), and
+//    the unguarded Hoare partition is evaluated in parallel: the k-th swap
+//    pairs the k-th element >= pivot from the left with the k-th element <=
+//    pivot from the right while they have not crossed, so ranks from two
+//    prefix sums (rounds of global scans) give every swap and the cut at once;
+//  * shorter segments run libstdc++'s introsort loop (heapsort at depth 0)
+//    and the final insertion sort in one thread each;
+//  * the final insertion sort never moves an element across a partition
+//    boundary, so sorting each leaf segment separately gives the same order.
+// The SAH sweeps (triangles_raytracing.cpp:53-98) are one workgroup per
+// (candidate, axis): a reverse scan for the right boxes, a forward scan for
+// the left boxes and the cost, and the first minimum. The breadth-first
+// candidate queue of createNode (:155-225, at most 7 splits) is driven from
+// the host, one candidate layer of every open node per stage; candidates the
+// reference never reaches once a node has 7 splits are evaluated
+// speculatively and rolled back (their range restored), because tryDivide
+// re-sorts its range even when it does not split.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtamd.h"
+#include "rt_error.h"
+#include "rt_host.h"
+#include "rt_layout.h"
+
+namespace {
+
+constexpr uint32_t kSerialMax = 1024;  // segments at most this long: one thread, serial introsort
+constexpr int kScanT = 256, kScanI = 8, kScanBlk = kScanT * kScanI;
+
+struct Seg {
+  uint32_t first, last;  // position range in the 3n-element space (axis a: [a*n, (a+1)*n))
+  int32_t depth;         // remaining introsort depth
+  uint32_t pad;
+};
+
+// ---- libstdc++'s sort algorithms on ids compared by K[id] ------------------
+__device__ __forceinline__ bool lt(const float *K, uint32_t a, uint32_t b) { return K[a] < K[b]; }
+__device__ __forceinline__ void d_swap(uint32_t *a, uint32_t *b) {
+  const uint32_t t = *a;
+  *a = *b;
+  *b = t;
+}
+// std::__insertion_sort
+__device__ void d_insertion(uint32_t *first, uint32_t *last, const float *K) {
+  if (first == last) return;
+  for (uint32_t *i = first + 1; i != last; ++i) {
+    const uint32_t v = *i;
+    if (lt(K, v, *first)) {
+      for (uint32_t *j = i; j != first; --j) *j = *(j - 1);
+      *first = v;
+    } else {  // std::__unguarded_linear_insert
+      uint32_t *l = i, *nx = i - 1;
+      while (lt(K, v, *nx)) {
+        *l = *nx;
+        l = nx;
+        --nx;
+      }
+      *l = v;
+    }
+  }
+}
+// std::__move_median_to_first
+__device__ void d_median_to_first(uint32_t *r, uint32_t *a, uint32_t *b, uint32_t *c, const float *K) {
+  if (lt(K, *a, *b)) {
+    if (lt(K, *b, *c)) d_swap(r, b);
+    else if (lt(K, *a, *c)) d_swap(r, c);
+    else d_swap(r, a);
+  } else if (lt(K, *a, *c)) d_swap(r, a);
+  else if (lt(K, *b, *c)) d_swap(r, c);
+  else d_swap(r, b);
+}
+// std::__unguarded_partition
+__device__ uint32_t *d_partition(uint32_t *first, uint32_t *last, uint32_t *pivot, const float *K) {
+  for (;;) {
+    while (lt(K, *first, *pivot)) ++first;
+    --last;
+    while (lt(K, *pivot, *last)) --last;
+    if (!(first < last)) return first;
+    d_swap(first, last);
+    ++first;
+  }
+}
+// std::__adjust_heap (with std::__push_heap)
+__device__ void d_adjust_heap(uint32_t *first, int64_t hole, int64_t len, uint32_t value, const float *K) {
+  const int64_t top = hole;
+  int64_t child = hole;
+  while (child < (len - 1) / 2) {
+    child = 2 * (child + 1);
+    if (lt(K, first[child], first[child - 1])) child--;
+    first[hole] = first[child];
+    hole = child;
+  }
+  if ((len & 1) == 0 && child == (len - 2) / 2) {
+    child = 2 * (child + 1);
+    first[hole] = first[child - 1];
+    hole = child - 1;
+  }
+  int64_t parent = (hole - 1) / 2;
+  while (hole > top && lt(K, first[parent], value)) {
+    first[hole] = first[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  first[hole] = value;
+}
+// std::__partial_sort(first, last, last): std::__make_heap, then std::__sort_heap
+__device__ void d_heapsort(uint32_t *first, uint32_t *last, const float *K) {
+  const int64_t len = last - first;
+  if (len >= 2) {
+    for (int64_t parent = (len - 2) / 2;; --parent) {
+      d_adjust_heap(first, parent, len, first[parent], K);
+      if (parent == 0) break;
+    }
+  }
+  while (last - first > 1) {  // std::__pop_heap(first, last - 1, last - 1)
+    --last;
+    const uint32_t v = *last;
+    *last = *first;
+    d_adjust_heap(first, 0, last - first, v, K);
+  }
+}
+// std::__introsort_loop, the recursion on the right part kept on a stack
+__device__ void d_introsort(uint32_t *first, uint32_t *last, int depth, const float *K) {
+  struct Fr {
+    uint32_t *f, *l;
+    int d;
+  } st[64];
+  int sp = 0;
+  for (;;) {
+    while (last - first > 16) {
+      if (depth == 0) {
+        d_heapsort(first, last, K);
+        break;
+      }
+      --depth;
+      uint32_t *mid = first + (last - first) / 2;
+      d_median_to_first(first, first + 1, mid, last - 1, K);
+      uint32_t *cut = d_partition(first + 1, last, first, K);
+      st[sp++] = Fr{cut, last, depth};
+      last = cut;
+    }
+    if (sp == 0) break;
+    --sp;
+    first = st[sp].f;
+    last = st[sp].l;
+    depth = st[sp].d;
+  }
+}
+
+// one thread per short segment: the rest of the introsort and the final insertion sort
+__global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t cnt, uint32_t *ids, const float *K3,
+                                                uint32_t n) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= cnt) return;
+  const Seg s = segs[i];
+  const float *K = K3 + (size_t)(s.first / n) * n;
+  d_introsort(ids + s.first, ids + s.last, s.depth, K);
+  d_insertion(ids + s.first, ids + s.last, K);
+}
+
+// ---- inclusive scan of u32 (three launches) --------------------------------
+__global__ __launch_bounds__(kScanT) void k_scan1(const uint32_t *in, uint32_t *out, uint32_t *bsum, uint32_t n) {
+  __shared__ uint32_t sm[kScanT];
+  const uint32_t base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
+  uint32_t v[kScanI], acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanI; ++k) {
+    acc += (base + k < n) ? in[base + k] : 0u;
+    v[k] = acc;
+  }
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 1; o < kScanT; o <<= 1) {
+    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sm[threadIdx.x] += x;
+    __syncthreads();
+  }
+  const uint32_t ex = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
+#pragma unroll
+  for (int k = 0; k < kScanI; ++k)
+    if (base + k < n) out[base + k] = v[k] + ex;
+  if (threadIdx.x == kScanT - 1) bsum[blockIdx.x] = sm[kScanT - 1];
+}
+__global__ __launch_bounds__(1024) void k_scan2(uint32_t *bsum, uint32_t nb) {
+  __shared__ uint32_t sm[1024];
+  const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < per; ++k)
+    if (b0 + k < nb) acc += bsum[b0 + k];
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sm[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
+  for (uint32_t k = 0; k < per; ++k)
+    if (b0 + k < nb) {
+      run += bsum[b0 + k];
+      bsum[b0 + k] = run;
+    }
+}
+__global__ __launch_bounds__(kScanT) void k_scan3(uint32_t *out, const uint32_t *bsum, uint32_t n) {
+  if (blockIdx.x == 0) return;
+  const uint32_t add = bsum[blockIdx.x - 1], base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
+#pragma unroll
+  for (int k = 0; k < kScanI; ++k)
+    if (base + k < n) out[base + k] += add;
+}
+
+// ---- one round of parallel introsort partitions ----------------------------
+// per segment: median to the front, pivot key, size (0: depth exhausted, the
+// segment goes to the serial list, whose introsort loop heapsorts it)
+__global__ void k_prep(const Seg *segs, uint32_t m, uint32_t *ids, const float *K3, uint32_t n, float *kp,
+                       uint32_t *size, Seg *serial, uint32_t *nserial) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const Seg s = segs[i];
+  if (s.depth == 0) {
+    serial[atomicAdd(nserial, 1u)] = s;
+    size[i] = 0;
+    return;
+  }
+  const float *K = K3 + (size_t)(s.first / n) * n;
+  uint32_t *f = ids + s.first, *l = ids + s.last;
+  d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, K);
+  kp[i] = K[*f];
+  size[i] = s.last - s.first;
+}
+
+__device__ __forceinline__ uint32_t seg_of(const uint32_t *offs, uint32_t m, uint32_t v) {
+  uint32_t lo = 0, hi = m;  // largest i with offs[i] <= v
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= v) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// flags over the active elements (virtual index v, segments back to back):
+// a = stops the left scan of the partition (!(key < pivot), the pivot itself
+// excluded), b = stops the right scan (!(pivot < key), the pivot included)
+__global__ void k_flags(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *ids, const float *K3,
+                        uint32_t n, const float *kp, uint32_t *af, uint32_t *bf, uint32_t *segv, uint32_t E) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= E || v >= offs[m]) return;  // E: host bound; offs[m]: elements of this round
+  const uint32_t i = seg_of(offs, m, v);
+  const Seg s = segs[i];
+  const uint32_t p = s.first + (v - offs[i]);
+  const float *K = K3 + (size_t)(s.first / n) * n;
+  const float k = K[ids[p]], pk = kp[i];
+  af[v] = (p != s.first && !(k < pk)) ? 1u : 0u;
+  bf[v] = (p == s.first || !(pk < k)) ? 1u : 0u;
+  segv[v] = i;
+}
+
+// ranks of the a-elements from the left and the b-elements from the right,
+// scattered into per-segment position lists L, R (v-space, offs[i] + rank - 1)
+__global__ void k_ranks(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af, const uint32_t *bf,
+                        const uint32_t *Ai, const uint32_t *Bi, const uint32_t *segv, uint32_t *Lpos,
+                        uint32_t *Rpos, uint32_t E) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= E || v >= offs[m]) return;
+  const uint32_t i = segv[v], o = offs[i], oe = offs[i + 1];
+  const uint32_t p = segs[i].first + (v - o);
+  const uint32_t abase = o ? Ai[o - 1] : 0u, bbase = o ? Bi[o - 1] : 0u;
+  if (af[v]) Lpos[o + (Ai[v] - abase) - 1] = p;
+  if (bf[v]) {
+    const uint32_t btot = Bi[oe - 1] - bbase;
+    Rpos[o + (btot - (Bi[v] - bbase) + 1) - 1] = p;
+  }
+}
+
+// number of swaps s: the a-element of rank k swaps with the b-element of rank
+// k from the right while it lies left of it, i.e. while at least k b-elements
+// lie strictly right of it (monotone in k); the a-element where that stops
+// writes s (one writer per segment; s stays 0 if the first one fails)
+__device__ __forceinline__ bool pred_at(const Seg &s, uint32_t o, uint32_t oe, uint32_t p, uint32_t rank,
+                                        const uint32_t *Bi) {
+  const uint32_t v = o + (p - s.first);
+  const uint32_t nright = Bi[oe - 1] - Bi[v];  // b-elements strictly right of p
+  return nright >= rank;
+}
+__global__ void k_swaps_count(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af,
+                              const uint32_t *Ai, const uint32_t *Bi, const uint32_t *segv, const uint32_t *Lpos,
+                              uint32_t *sw, uint32_t E) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= E || v >= offs[m] || !af[v]) return;
+  const uint32_t i = segv[v], o = offs[i], oe = offs[i + 1];
+  const Seg s = segs[i];
+  const uint32_t abase = o ? Ai[o - 1] : 0u, na = Ai[oe - 1] - abase, rank = Ai[v] - abase;
+  const uint32_t p = s.first + (v - o);
+  if (!pred_at(s, o, oe, p, rank, Bi)) return;
+  if (rank == na || !pred_at(s, o, oe, Lpos[o + rank], rank + 1, Bi)) sw[i] = rank;
+}
+
+// the swaps themselves: one thread per pair (its a-element)
+__global__ void k_swap(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af, const uint32_t *Ai,
+                       const uint32_t *segv, const uint32_t *Rpos, const uint32_t *sw, uint32_t *ids, uint32_t E) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= E || v >= offs[m] || !af[v]) return;
+  const uint32_t i = segv[v], o = offs[i];
+  const uint32_t rank = Ai[v] - (o ? Ai[o - 1] : 0u);
+  if (rank > sw[i]) return;
+  const uint32_t p = segs[i].first + (v - o), q = Rpos[o + rank - 1];
+  d_swap(ids + p, ids + q);
+}
+
+// the cut (where the left scan stops after the last swap) and the two parts:
+// longer than kSerialMax -> next round, else the serial list
+__global__ void k_split(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *size, const uint32_t *Ai,
+                        const uint32_t *Lpos, const uint32_t *Rpos, const uint32_t *sw, Seg *next,
+                        uint32_t *nnext, uint32_t *Enext, Seg *serial, uint32_t *nserial) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m || size[i] == 0) return;
+  const Seg s = segs[i];
+  const uint32_t o = offs[i], oe = offs[i + 1];
+  const uint32_t na = Ai[oe - 1] - (o ? Ai[o - 1] : 0u), k = sw[i];
+  uint32_t cut;
+  if (k == 0) cut = Lpos[o];  // the median of three guarantees an element >= pivot
+  else {
+    const uint32_t rk = Rpos[o + k - 1];
+    cut = (k < na) ? min(Lpos[o + k], rk) : rk;
+  }
+  const Seg parts[2] = {Seg{cut, s.last, s.depth - 1, 0}, Seg{s.first, cut, s.depth - 1, 0}};
+  for (const Seg &q : parts) {
+    if (q.last - q.first > kSerialMax) {
+      next[atomicAdd(nnext, 1u)] = q;
+      atomicAdd(Enext, q.last - q.first);
+    } else if (q.last - q.first > 1) {
+      serial[atomicAdd(nserial, 1u)] = q;
+    }
+  }
+}
+
+// ---- SAH sweeps: one workgroup per (candidate, axis) -----------------------
+struct TBox {
+  float mn[3], mx[3];
+};
+__device__ __forceinline__ TBox tb_empty() {
+  const float inf = __builtin_huge_valf();
+  return TBox{{inf, inf, inf}, {-inf, -inf, -inf}};
+}
+// std::min / std::max as the reference's update_box / calc_bbox use them
+__device__ __forceinline__ TBox tb_union(const TBox &a, const TBox &b) {
+  TBox r;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    r.mn[k] = (b.mn[k] < a.mn[k]) ? b.mn[k] : a.mn[k];
+    r.mx[k] = (a.mx[k] < b.mx[k]) ? b.mx[k] : a.mx[k];
+  }
+  return r;
+}
+__device__ __forceinline__ float tb_area(const TBox &b) {  // surfaceArea (raytracing.hpp:62-65)
+  const float dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+  return 2 * (dx * dy + dx * dz + dy * dz);
+}
+
+constexpr int kSahT = 256;
+// inclusive scan of box unions over the block; dir = +1: thread order, -1: reverse
+__device__ TBox block_scan_box(TBox b, TBox *sm) {
+  sm[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 1; o < kSahT; o <<= 1) {
+    TBox x = tb_empty();
+    if (threadIdx.x >= (uint32_t)o) x = sm[threadIdx.x - o];
+    __syncthreads();
+    sm[threadIdx.x] = tb_union(x, sm[threadIdx.x]);
+    __syncthreads();
+  }
+  return sm[threadIdx.x];
+}
+
+struct Task {
+  uint32_t s, e;  // triangle range [s, e) of one candidate
+};
+
+__global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t *ids3, const TBox *tbox, uint32_t n,
+                                               TBox *rightB3, float *out_cost, uint32_t *out_div) {
+  __shared__ TBox sm[kSahT];
+  __shared__ float s_psa;
+  __shared__ float s_cost[kSahT];
+  __shared__ uint32_t s_div[kSahT];
+  const Task tk = tasks[blockIdx.x / 3];
+  const uint32_t base = (blockIdx.x % 3) * n;
+  const uint32_t *ids = ids3 + base;
+  TBox *rightB = rightB3 + base;
+  // right boxes: union over [t, e), built from the end (triangles_raytracing.cpp:67-80)
+  TBox carry = tb_empty();
+  for (int64_t hi = tk.e; hi > (int64_t)tk.s; hi -= kSahT) {
+    const int64_t t = hi - 1 - (int64_t)threadIdx.x;
+    const TBox b = (t >= (int64_t)tk.s) ? tbox[ids[t]] : tb_empty();
+    const TBox r = tb_union(carry, block_scan_box(b, sm));
+    if (t >= (int64_t)tk.s) rightB[t] = r;
+    const TBox tot = sm[kSahT - 1];
+    __syncthreads();
+    carry = tb_union(carry, tot);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) s_psa = tb_area(rightB[tk.s]);  // parent box (:84)
+  __syncthreads();
+  const float psa = s_psa;
+  // left boxes and the cost of every divider (:85-98); first minimum
+  float best = __builtin_huge_valf();
+  uint32_t bdiv = 0xFFFFFFFFu;
+  carry = tb_empty();
+  for (uint32_t lo = tk.s; lo < tk.e; lo += kSahT) {
+    const uint32_t t = lo + threadIdx.x;
+    const TBox b = (t < tk.e) ? tbox[ids[t]] : tb_empty();
+    const TBox left = tb_union(carry, block_scan_box(b, sm));
+    const TBox tot = sm[kSahT - 1];
+    const uint32_t d = t + 1;  // divider after triangle t (index units: 3 d)
+    if (d < tk.e) {
+      const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
+      const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
+      const float c = 0.2f + tb_area(left) / psa * lc + tb_area(rightB[d]) / psa * rc;
+      if (c < best) {  // NaN never wins, as `curSAH < result.sah`
+        best = c;
+        bdiv = d;
+      }
+    }
+    __syncthreads();
+    carry = tb_union(carry, tot);
+  }
+  s_cost[threadIdx.x] = best;
+  s_div[threadIdx.x] = bdiv;
+  __syncthreads();
+  for (int o = kSahT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < (uint32_t)o) {
+      const float c2 = s_cost[threadIdx.x + o];
+      const uint32_t d2 = s_div[threadIdx.x + o];
+      if (c2 < s_cost[threadIdx.x] || (c2 == s_cost[threadIdx.x] && d2 < s_div[threadIdx.x])) {
+        s_cost[threadIdx.x] = c2;
+        s_div[threadIdx.x] = d2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out_cost[blockIdx.x] = s_cost[0];
+    out_div[blockIdx.x] = s_div[0];
+  }
+}
+
+// stage start: every candidate range saved (rollback) and copied to the Y / Z scratch
+__global__ void k_stage_copy(const Task *tasks, uint32_t *ids3, uint32_t *backup, uint32_t n) {
+  const Task tk = tasks[blockIdx.x];
+  for (uint32_t t = tk.s + threadIdx.x; t < tk.e; t += blockDim.x) {
+    const uint32_t v = ids3[t];
+    backup[t] = v;
+    ids3[n + t] = v;
+    ids3[2 * n + t] = v;
+  }
+}
+// stage end: 1 = take the Y order, 2 = the Z order, 3 = restore (never evaluated by the reference)
+__global__ void k_stage_apply(const Task *tasks, const uint32_t *action, uint32_t *ids3, const uint32_t *backup,
+                              uint32_t n) {
+  const Task tk = tasks[blockIdx.x];
+  const uint32_t a = action[blockIdx.x];
+  if (a == 0) return;
+  const uint32_t *src = a == 1 ? ids3 + n : a == 2 ? ids3 + 2 * n : backup;
+  for (uint32_t t = tk.s + threadIdx.x; t < tk.e; t += blockDim.x) ids3[t] = src[t];
+}
+
+// per-triangle box (calc_bbox of the /w-divided vertices, raytracing.hpp:51-60) and keys
+__global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TBox *tbox, float *K3) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  TBox b = tb_empty();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float4 v = vpos[idx[3 * t + k]];
+    const float x = v.x / v.w, y = v.y / v.w, z = v.z / v.w;
+    b = tb_union(b, TBox{{x, y, z}, {x, y, z}});
+  }
+  tbox[t] = b;
+  K3[t] = b.mx[0];
+  K3[n + t] = b.mx[1];
+  K3[2 * n + t] = b.mx[2];
+}
+
+// child boxes: union over a final triangle range (calc_bbox(m_mesh, lo, hi), :199)
+__global__ __launch_bounds__(kSahT) void k_range_box(const Task *ranges, const uint32_t *ids, const TBox *tbox,
+                                                     TBox *out) {
+  __shared__ TBox sm[kSahT];
+  const Task r = ranges[blockIdx.x];
+  // contiguous chunks, combined in order: among equal bounds (+0 / -0) the
+  // first in range order is kept, as the sequential std::min / std::max do
+  const uint32_t len = r.e - r.s, per = (len + kSahT - 1) / kSahT;
+  const uint32_t t0 = r.s + threadIdx.x * per, t1 = min(r.e, t0 + per);
+  TBox acc = tb_empty();
+  for (uint32_t t = t0; t < t1; ++t) acc = tb_union(acc, tbox[ids[t]]);
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = kSahT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < (uint32_t)o) sm[threadIdx.x] = tb_union(sm[threadIdx.x], sm[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
+}
+
+// ---- host side ---------------------------------------------------------------
+template <class T>
+struct DBuf {
+  T *p = nullptr;
+  size_t cap = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int reserve(size_t n) {
+    if (n <= cap) return RT_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    cap = n;
+    return RT_OK;
+  }
+};
+
+inline int lg2(uint64_t n) { return 63 - __builtin_clzll(n); }
+
+struct Sorter {
+  uint32_t n = 0;  // triangles (one axis block of the 3n space)
+  uint32_t *ids = nullptr;
+  const float *K3 = nullptr;
+  DBuf<Seg> segA, segB, serial;
+  DBuf<uint32_t> size, offs, sw, af, bf, Ai, Bi, segv, Lpos, Rpos, bsum, ctr;
+  DBuf<float> kp;
+  hipStream_t st = nullptr;
+
+  int init(uint32_t ntri, uint32_t *ids3, const float *keys3) {
+    n = ntri;
+    ids = ids3;
+    K3 = keys3;
+    const size_t N = 3 * (size_t)n, segcap = N / kSerialMax + 16, sercap = N / 2 + 4096;
+    int rc;
+    if ((rc = segA.reserve(segcap)) || (rc = segB.reserve(segcap)) || (rc = serial.reserve(sercap)) ||
+        (rc = size.reserve(segcap + 1)) || (rc = offs.reserve(segcap + 1)) || (rc = sw.reserve(segcap)) ||
+        (rc = kp.reserve(segcap)) || (rc = af.reserve(N)) || (rc = bf.reserve(N)) || (rc = Ai.reserve(N)) ||
+        (rc = Bi.reserve(N)) || (rc = segv.reserve(N)) || (rc = Lpos.reserve(N)) || (rc = Rpos.reserve(N)) ||
+        (rc = bsum.reserve(N / kScanBlk + 2)) || (rc = ctr.reserve(4)))
+      return rc;
+    return RT_OK;
+  }
+
+  int scan(const uint32_t *in, uint32_t *out, uint32_t cnt) {
+    if (cnt == 0) return RT_OK;
+    const uint32_t nb = (cnt + kScanBlk - 1) / kScanBlk;
+    k_scan1<<<nb, kScanT, 0, st>>>(in, out, bsum.p, cnt);
+    if (nb > 1) {
+      k_scan2<<<1, 1024, 0, st>>>(bsum.p, nb);
+      k_scan3<<<nb, kScanT, 0, st>>>(out, bsum.p, cnt);
+    }
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+  }
+
+  // sort every segment of `init` (host list): exactly std::sort on each
+  int sort(const std::vector<Seg> &init) {
+    std::vector<Seg> act, ser;
+    for (const Seg &s : init) {
+      if (s.last - s.first <= 1) continue;
+      (s.last - s.first > kSerialMax ? act : ser).push_back(s);
+    }
+    uint32_t nser = (uint32_t)ser.size(), m = (uint32_t)act.size(), E = 0;
+    for (const Seg &s : act) E += s.last - s.first;
+    if (nser) HIP_TRY(hipMemcpyAsync(serial.p, ser.data(), nser * sizeof(Seg), hipMemcpyHostToDevice, st));
+    if (m) HIP_TRY(hipMemcpyAsync(segA.p, act.data(), m * sizeof(Seg), hipMemcpyHostToDevice, st));
+    uint32_t hc[3] = {0, 0, nser};  // next count, next E, serial count
+    HIP_TRY(hipMemcpyAsync(ctr.p + 2, &hc[2], 4, hipMemcpyHostToDevice, st));
+    Seg *cur = segA.p, *nxt = segB.p;
+    while (m > 0) {
+      HIP_TRY(hipMemsetAsync(ctr.p, 0, 8, st));
+      HIP_TRY(hipMemsetAsync(sw.p, 0, (size_t)m * 4, st));
+      const uint32_t gm = (m + 255) / 256;
+      k_prep<<<gm, 256, 0, st>>>(cur, m, ids, K3, n, kp.p, size.p + 1, serial.p, ctr.p + 2);
+      HIP_TRY(hipMemsetAsync(size.p, 0, 4, st));
+      if (int rc = scan(size.p, offs.p, m + 1)) return rc;  // offs[i] = sum of sizes before segment i
+      const uint32_t ge = (E + 255) / 256;
+      if (E) {
+        k_flags<<<ge, 256, 0, st>>>(cur, offs.p, m, ids, K3, n, kp.p, af.p, bf.p, segv.p, E);
+        if (int rc = scan(af.p, Ai.p, E)) return rc;
+        if (int rc = scan(bf.p, Bi.p, E)) return rc;
+        k_ranks<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, bf.p, Ai.p, Bi.p, segv.p, Lpos.p, Rpos.p, E);
+        k_swaps_count<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, Bi.p, segv.p, Lpos.p, sw.p, E);
+        k_swap<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, segv.p, Rpos.p, sw.p, ids, E);
+        k_split<<<gm, 256, 0, st>>>(cur, offs.p, m, size.p + 1, Ai.p, Lpos.p, Rpos.p, sw.p, nxt, ctr.p, ctr.p + 1,
+                                    serial.p, ctr.p + 2);
+      }
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(hc, ctr.p, 12, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      m = hc[0];
+      E = hc[1];
+      std::swap(cur, nxt);
+    }
+    HIP_TRY(hipMemcpyAsync(&nser, ctr.p + 2, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (nser) k_serial<<<(nser + 63) / 64, 64, 0, st>>>(serial.p, nser, ids, K3, n);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+  }
+};
+
+// BVHBuilder::createNode state of one node (triangles_raytracing.cpp:155-225)
+struct Open {
+  int32_t node;
+  uint32_t start, end;  // index units
+  std::vector<std::pair<uint32_t, uint32_t>> queue;  // ChipQueue contents, FIFO
+  uint32_t div[8];
+  int nd = 0;
+};
+
+}  // namespace
+
+namespace rth {
+
+bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                    std::string &err) {
+  auto fail = [&](const char *what) {
+    err = std::string("GPU BVH build: ") + what + ": " + rterr::get();
+    return false;
+  };
+  if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
+  for (int64_t i = 0; i < nidx; ++i)
+    if ((int64_t)idx[i] >= nverts) { err = "vertex index out of range"; return false; }
+  const uint32_t n = (uint32_t)(nidx / 3);
+  if ((uint64_t)n > rtl::kMaxLeafFirstTri || 3ull * n >= (1ull << 31)) { err = "too many triangles"; return false; }
+  out = BVHGpu();
+  if (n == 0) { out.root_word = rtl::kInvalidChild; return true; }
+
+  DBuf<float4> dv;
+  DBuf<uint32_t> didx, ids3, backup, ddiv, dact;
+  DBuf<float> K3, dcost;
+  DBuf<TBox> tbox, rightB3, boxes;
+  DBuf<Task> dtasks;
+  Sorter S;
+  if (dv.reserve((size_t)nverts) || didx.reserve((size_t)nidx) || ids3.reserve(3 * (size_t)n) ||
+      backup.reserve(n) || K3.reserve(3 * (size_t)n) || tbox.reserve(n) || rightB3.reserve(3 * (size_t)n) ||
+      S.init(n, nullptr, nullptr))
+    return fail("allocation");
+  S.ids = ids3.p;
+  S.K3 = K3.p;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return false; }
+  S.st = st;
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() { (void)hipStreamDestroy(s); }
+  } sg{st};
+  std::vector<uint32_t> iota(n);
+  for (uint32_t t = 0; t < n; ++t) iota[t] = t;
+  if (hipMemcpyAsync(dv.p, vpos4, (size_t)nverts * 16, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(didx.p, idx, (size_t)nidx * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+    err = "upload";
+    return false;
+  }
+  k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p);
+
+  std::vector<BvhHostNode> H(1);
+  std::vector<Open> open;
+  open.push_back(Open{0, 0, 3 * n, {{0u, 3 * n}}, {}, 0});
+  std::vector<Task> ranges;   // child ranges (triangle units) for the final boxes
+  std::vector<std::pair<int32_t, int>> range_of;  // (node, child slot) per range
+  while (!open.empty()) {
+    // this stage: every queued candidate of every open node that tryDivide sorts (> 8 triangles)
+    std::vector<Task> tasks;
+    std::vector<std::vector<int>> task_of(open.size());
+    for (size_t o = 0; o < open.size(); ++o)
+      for (auto &c : open[o].queue) {
+        const bool gpu = c.second - c.first > 24;
+        task_of[o].push_back(gpu ? (int)tasks.size() : -1);
+        if (gpu) tasks.push_back(Task{c.first / 3, c.second / 3});
+      }
+    const uint32_t T = (uint32_t)tasks.size();
+    std::vector<float> cost(3 * (size_t)T);
+    std::vector<uint32_t> dvd(3 * (size_t)T), action(T, 0);
+    if (T) {
+      if (dtasks.reserve(T) || dcost.reserve(3 * (size_t)T) || ddiv.reserve(3 * (size_t)T) || dact.reserve(T))
+        return fail("allocation");
+      if (hipMemcpyAsync(dtasks.p, tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st) != hipSuccess) {
+        err = "upload";
+        return false;
+      }
+      k_stage_copy<<<T, 256, 0, st>>>(dtasks.p, ids3.p, backup.p, n);
+      std::vector<Seg> segs;
+      segs.reserve(3 * (size_t)T);
+      for (int a = 0; a < 3; ++a)
+        for (const Task &tk : tasks)
+          segs.push_back(Seg{a * n + tk.s, a * n + tk.e, 2 * lg2(tk.e - tk.s), 0});
+      if (S.sort(segs)) return fail("sort");
+      k_sah<<<3 * T, kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, n, rightB3.p, dcost.p, ddiv.p);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(cost.data(), dcost.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(dvd.data(), ddiv.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        err = "SAH sweep";
+        return false;
+      }
+    }
+    // createNode's FIFO, candidate by candidate (triangles_raytracing.cpp:162-173)
+    std::vector<Open> next;
+    for (size_t o = 0; o < open.size(); ++o) {
+      Open &N = open[o];
+      std::vector<std::pair<uint32_t, uint32_t>> q2;
+      bool capped = false;
+      for (size_t c = 0; c < N.queue.size(); ++c) {
+        const auto cand = N.queue[c];
+        const int ti = task_of[o][c];
+        if (N.nd == 7) {  // the reference stops here: this candidate is never tried
+          capped = true;
+          if (ti >= 0) action[ti] = 3;
+          continue;
+        }
+        if (ti < 0) continue;  // <= 8 triangles: tryDivide returns at once
+        // tryDivide(start, end) (:119-153) from the three tryDivide(indices, start, end, axis)
+        const uint32_t start = cand.first, end = cand.second;
+        const float curSAH = static_cast<float>(end - start) / 3.0f;
+        float sah[3];
+        bool divided[3];
+        uint32_t dv3[3];
+        for (int a = 0; a < 3; ++a) {
+          const float cst = cost[(size_t)3 * ti + a];
+          divided[a] = cst < curSAH;
+          sah[a] = divided[a] ? cst : curSAH;
+          uint32_t d = dvd[(size_t)3 * ti + a] * 3;
+          if (divided[a] && (d - start) % 24 != 0) {  // align to 8 (:100-114)
+            const uint32_t d1 = (d - 1) / 24 * 24, d2 = ((d - 1) / 24 + 1) * 24;
+            const uint32_t nearest = (d - d1 <= d2 - d) ? d1 : d2, other = d1 + d2 - nearest;
+            if (start < nearest && nearest < end) d = nearest;
+            else if (start < other && other < end) d = other;
+          }
+          dv3[a] = d;
+        }
+        const float mn = std::min({curSAH, sah[0], sah[1], sah[2]});
+        int win = -1;
+        if (sah[0] == mn) win = 0;
+        else if (sah[1] == mn) win = 1;
+        else if (sah[2] == mn) win = 2;
+        action[ti] = win == 1 ? 1u : win == 2 ? 2u : 0u;
+        if (win >= 0 && divided[win]) {
+          N.div[N.nd++] = dv3[win];
+          q2.push_back({start, dv3[win]});
+          q2.push_back({dv3[win], end});
+        }
+      }
+      N.queue = (capped || N.nd == 7) ? std::vector<std::pair<uint32_t, uint32_t>>{} : q2;
+      if (!N.queue.empty()) {
+        next.push_back(std::move(N));
+        continue;
+      }
+      // node complete (:175-224)
+      BvhHostNode node;
+      if (N.nd == 0) {
+        if (N.end - N.start > 24) {
+          N.div[N.nd++] = ((N.start / 3 + N.end / 3) / 2) * 3;
+        } else {
+          node.leaf = true;
+          node.start = N.start;
+          node.count = N.end - N.start;
+          H[N.node] = node;
+          continue;
+        }
+      }
+      std::sort(N.div, N.div + N.nd);
+      node.nchild = (uint32_t)(N.nd + 1);
+      for (int c = 0; c <= N.nd; ++c) {
+        const uint32_t lo = c == 0 ? N.start : N.div[c - 1], hi = c == N.nd ? N.end : N.div[c];
+        node.child[c] = (int32_t)H.size();
+        H.emplace_back();
+        ranges.push_back(Task{lo / 3, hi / 3});
+        range_of.push_back({N.node, c});
+        next.push_back(Open{node.child[c], lo, hi, {{lo, hi}}, {}, 0});
+      }
+      H[N.node] = node;
+    }
+    if (T) {
+      if (hipMemcpyAsync(dact.p, action.data(), T * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+        err = "upload";
+        return false;
+      }
+      k_stage_apply<<<T, 256, 0, st>>>(dtasks.p, dact.p, ids3.p, backup.p, n);
+      if (hipGetLastError() != hipSuccess) { err = "stage apply"; return false; }
+    }
+    open.swap(next);
+  }
+  // child boxes over the final triangle order, and the order itself
+  std::vector<uint32_t> cur(n);
+  if (!ranges.empty()) {
+    if (dtasks.reserve(ranges.size()) || boxes.reserve(ranges.size())) return fail("allocation");
+    std::vector<TBox> hb(ranges.size());
+    if (hipMemcpyAsync(dtasks.p, ranges.data(), ranges.size() * sizeof(Task), hipMemcpyHostToDevice, st) !=
+        hipSuccess) {
+      err = "upload";
+      return false;
+    }
+    k_range_box<<<(uint32_t)ranges.size(), kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, boxes.p);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(hb.data(), boxes.p, hb.size() * sizeof(TBox), hipMemcpyDeviceToHost, st) != hipSuccess) {
+      err = "child boxes";
+      return false;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) { err = "child boxes"; return false; }
+    for (size_t r = 0; r < ranges.size(); ++r) {
+      BvhBox &b = H[range_of[r].first].box[range_of[r].second];
+      std::memcpy(b.mn, hb[r].mn, 12);
+      std::memcpy(b.mx, hb[r].mx, 12);
+    }
+  }
+  if (hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    err = "download";
+    return false;
+  }
+  bvh_layout(vpos4, idx, nidx, H, cur, out);
+  return true;
+}
+
+}  // namespace rth
+
+// ---- diagnostics (not part of include/rtamd.h) ------------------------------
+extern "C" {
+
+// The device sort against libstdc++ std::sort (host_introsort) on n keys:
+// ids[] receives the device permutation; returns RT_OK and *mismatch = number
+// of positions that differ from the host permutation. depth < 0: std::sort's
+// own depth limit (2 lg n); smaller limits force the heapsort fallback.
+int rtx_sort_check(const float *keys, int64_t n, int32_t depth, uint32_t *ids_out, int64_t *mismatch) {
+  if (!keys || n <= 0 || n >= (1ll << 30) || !mismatch) return rterr::set(RT_E_INVALID, "bad arguments");
+  const uint32_t nn = (uint32_t)n;
+  std::vector<uint32_t> host(nn);
+  for (uint32_t i = 0; i < nn; ++i) host[i] = i;
+  rth::host_introsort(host.data(), nn, keys, depth);
+  // the sort works on a 3n space; the test uses axis block 0 only
+  DBuf<uint32_t> ids3;
+  DBuf<float> K3;
+  Sorter S;
+  if (int rc = ids3.reserve(3 * (size_t)nn)) return rc;
+  if (int rc = K3.reserve(3 * (size_t)nn)) return rc;
+  if (int rc = S.init(nn, ids3.p, K3.p)) return rc;
+  HIP_TRY(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+  std::vector<uint32_t> iota(nn);
+  for (uint32_t i = 0; i < nn; ++i) iota[i] = i;
+  int rc = RT_OK;
+  if (hipMemcpy(ids3.p, iota.data(), (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(K3.p, keys, (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess)
+    rc = rterr::set(RT_E_DEVICE, "upload");
+  if (!rc) rc = S.sort({Seg{0, nn, depth < 0 ? 2 * lg2(nn) : depth, 0}});
+  std::vector<uint32_t> dev(nn);
+  if (!rc && (hipStreamSynchronize(S.st) != hipSuccess ||
+              hipMemcpy(dev.data(), ids3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = rterr::set(RT_E_DEVICE, "download");
+  (void)hipStreamDestroy(S.st);
+  if (rc) return rc;
+  int64_t bad = 0;
+  for (uint32_t i = 0; i < nn; ++i) bad += dev[i] != host[i];
+  *mismatch = bad;
+  if (ids_out) std::memcpy(ids_out, dev.data(), (size_t)nn * 4);
+  return RT_OK;
+}
+
+}  // extern "C"

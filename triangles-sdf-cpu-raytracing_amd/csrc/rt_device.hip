@@ -1369,6 +1369,25 @@ void launch_rays_t(const S &sc, const PlaneDev &pl, const float *o, const float 
 }  // namespace
 
 namespace {
+// BVH8 builder selection (rt_set_bvh_builder): both builders give the same tree
+int g_bvh_mode = RT_BVH_AUTO;
+constexpr int64_t kBvhDeviceMinTris = 131072;  // auto: the device builder from this many triangles
+
+int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, rth::BVHGpu &b) {
+  std::string err;
+  int ndev = 0;
+  const bool dev = g_bvh_mode == RT_BVH_DEVICE ||
+                   (g_bvh_mode == RT_BVH_AUTO && nidx / 3 >= kBvhDeviceMinTris &&
+                    hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0);
+  if (dev) {
+    if (!rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err))
+      return set_err(err.rfind("GPU BVH build", 0) == 0 ? RT_E_DEVICE : RT_E_INVALID, err);
+    return RT_OK;
+  }
+  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  return RT_OK;
+}
+
 int new_scene(rt_scene **out) {
   if (!out) return set_err(RT_E_INVALID, "out is NULL");
   int dev = 0;
@@ -1470,12 +1489,17 @@ int rt_camera(const float pos[3], const float target[3], const float up[3], floa
   return RT_OK;
 }
 
+int rt_set_bvh_builder(int mode) {
+  if (mode < RT_BVH_AUTO || mode > RT_BVH_DEVICE) return set_err(RT_E_INVALID, "bad BVH builder mode");
+  g_bvh_mode = mode;
+  return RT_OK;
+}
+
 int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
                   uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth) {
   if (!vpos4 || !idx || !nnodes || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "bad mesh");
   rth::BVHGpu b;
-  std::string err;
-  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b)) return rc;
   const int64_t n = (int64_t)b.canon.size() / 52;
   if (canon) {
     if (*nnodes < n) return set_err(RT_E_INVALID, "buffer too small");
@@ -1491,8 +1515,7 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
                          rt_scene **out) {
   if (!vpos4 || !idx || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "empty mesh");
   rth::BVHGpu b;
-  std::string err;
-  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b)) return rc;
   int32_t maxd = 8;
   int rc = pick_maxd(b.max_depth, maxd);
   if (rc) return rc;

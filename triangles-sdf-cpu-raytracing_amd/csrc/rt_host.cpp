@@ -198,9 +198,7 @@ bool load_octree(const char *path, std::vector<uint8_t> &nodes36, std::string &e
 // renumbered afterwards (the reference's OpenMP task order only moves offsets).
 namespace {
 
-struct Box {
-  float mn[3], mx[3];
-};
+using Box = BvhBox;
 static inline Box empty_box() { return {{kInf, kInf, kInf}, {-kInf, -kInf, -kInf}}; }
 static inline void grow(Box &b, const Box &t) {
   for (int k = 0; k < 3; ++k) {
@@ -213,13 +211,7 @@ static inline float surface_area(const Box &b) {  // raytracing.hpp:62-65
   return 2 * (dx * dy + dx * dz + dy * dz);
 }
 
-struct HNode {
-  bool leaf = false;
-  uint32_t start = 0, count = 0;  // leaf: range in indices (reference units)
-  uint32_t nchild = 0;
-  int32_t child[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-  Box box[8];
-};
+using HNode = BvhHostNode;
 
 // std::sort, in parallel, with the exact permutation libstdc++'s serial
 // std::sort produces (introsort: median-of-three pivot moved to the front,
@@ -312,6 +304,20 @@ void sort(uint32_t *first, uint32_t *last, const float *K) {
   loop(first, last, 2 * lg(last - first), c);
 }
 }  // namespace psort
+
+}  // namespace
+
+// libstdc++'s std::sort on ids by keys K (the permutation the build depends
+// on), with an explicit depth limit (< 0: std::sort's own 2 * lg(n)); the host
+// reference of the device sort (tests via rtx_sort_check).
+void host_introsort(uint32_t *ids, size_t n, const float *K, int64_t depth_limit) {
+  if (n < 2) return;
+  psort::Less c{K};
+  psort::loop(ids, ids + n, depth_limit < 0 ? 2 * psort::lg((ptrdiff_t)n) : (ptrdiff_t)depth_limit, c);
+  psort::insertion(ids, ids + n, c);
+}
+
+namespace {
 
 struct Builder {
   std::vector<uint32_t> cur, scrY, scrZ;  // triangle ids, 'cur' = mesh.indices order
@@ -507,14 +513,18 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     B.create(0, 0, (size_t)nidx);
   }
 
-  // ---- canonical export + GPU layout (BFS over inner nodes) -------------
-  const std::vector<HNode> &H = B.nodes;
+  bvh_layout(vpos4, idx, nidx, B.nodes, B.cur, out);
+  return true;
+}
+
+void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
+                const std::vector<uint32_t> &cur, BVHGpu &out) {
+  const size_t ntri = (size_t)nidx / 3;
   out.host_nodes = (int64_t)H.size();
-  out.perm_tri = B.cur;
+  out.perm_tri = cur;
   out.perm_idx.resize((size_t)nidx);
   for (size_t t = 0; t < ntri; ++t)
-    for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)B.cur[t] + k];
-
+    for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)cur[t] + k];
   {  // canonical pre-order (52 u32 per node), same as the oracle's export
     std::vector<int32_t> st{0};
     while (!st.empty()) {
@@ -548,7 +558,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     const uint32_t nt = n.count / 3;
     for (uint32_t k = 0; k < nt; ++k) {
       const uint32_t slot = n.start / 3 + k;
-      const uint32_t *tv = idx + 3 * (size_t)B.cur[slot];
+      const uint32_t *tv = idx + 3 * (size_t)cur[slot];
       float v[3][3];
       for (int j = 0; j < 3; ++j) {
         const float *p = vpos4 + 4 * (size_t)tv[j];
@@ -557,7 +567,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
       }
       rtl::GTri g;
       g.v0x = v[0][0]; g.v0y = v[0][1]; g.v0z = v[0][2];
-      g.orig_id = B.cur[slot];
+      g.orig_id = cur[slot];
       g.e1x = v[1][0] - v[0][0]; g.e1y = v[1][1] - v[0][1]; g.e1z = v[1][2] - v[0][2];
       g.e2x = v[2][0] - v[0][0]; g.e2y = v[2][1] - v[0][1]; g.e2z = v[2][2] - v[0][2];
       g.pad1 = g.pad2 = 0.0f;
@@ -571,7 +581,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     out.root_word = leaf_word(H[0]);
     out.max_depth = 0;
     out.host_inner = 0;
-    return true;
+    return;
   }
   // BFS over inner nodes; depth = number of inner ancestors incl. itself
   std::vector<int32_t> order{0};
@@ -613,7 +623,6 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     for (uint32_t c = 0; c < r.nchild; ++c) grow(u, r.box[c]);
     for (int k = 0; k < 3; ++k) { out.root_box[k] = u.mn[k]; out.root_box[3 + k] = u.mx[k]; }
   }
-  return true;
 }
 
 // --------------------------------------------------------------- octree ---

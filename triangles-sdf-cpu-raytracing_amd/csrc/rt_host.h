@@ -36,6 +36,30 @@ struct BVHGpu {
 bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
                 std::string &err);
 
+// The tree BVHBuilder::perform builds (triangles_raytracing.cpp:155-225), as
+// either builder produces it: nodes (node 0 = root; children anywhere) and the
+// final triangle order (BVHBuilder's reordered mesh.indices / 3).
+struct BvhBox {
+  float mn[3], mx[3];
+};
+struct BvhHostNode {
+  bool leaf = false;
+  uint32_t start = 0, count = 0;  // leaf: range in indices (reference units)
+  uint32_t nchild = 0;
+  int32_t child[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  BvhBox box[8];
+};
+// libstdc++ std::sort of ids by K[id] (< 0 depth: std::sort's own limit).
+void host_introsort(uint32_t *ids, size_t n, const float *K, int64_t depth_limit);
+// Canonical export + GPU layout (GNode / GTri, BFS over inner nodes) of a built tree.
+void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
+                const std::vector<uint32_t> &cur, BVHGpu &out);
+// The same tree built on the current HIP device (rt_bvhgpu.hip): libstdc++'s
+// introsort replicated with parallel Hoare partitions, SAH sweeps as device
+// scans. Identical output to build_bvh8.
+bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                    std::string &err);
+
 struct OctGpu {
   std::vector<rtl::OctWord> child;    // per node: {0 leaf, kOctNeverHits or childrenOffset; child masks}
   std::vector<rtl::OctVals> vals;     // per node corner values

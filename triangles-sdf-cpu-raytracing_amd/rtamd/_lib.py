@@ -67,6 +67,7 @@ _SIGS = {
                             C.c_float, C.c_void_p, C.c_void_p]),
     "rt_bvh_export": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
                                 C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int32)]),
+    "rt_set_bvh_builder": (C.c_int, [C.c_int]),
     "rt_scene_create_mesh": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                        C.POINTER(C.c_void_p)]),
     "rt_scene_create_grid": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
