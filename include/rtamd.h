@@ -123,7 +123,8 @@ int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64
  * (src/triangles_raytracing.cpp:12-258): RT_BVH_HOST (OpenMP on the host),
  * RT_BVH_DEVICE (on the current HIP device: libstdc++'s introsort replicated
  * with parallel partitions, SAH sweeps as device scans) or RT_BVH_AUTO (the
- * device from 131,072 triangles). Both give the identical tree. Process-wide. */
+ * device from 32,768 triangles when a device is visible). Both give the
+ * identical tree. Process-wide. */
 enum rt_bvh_builder { RT_BVH_AUTO = 0, RT_BVH_HOST = 1, RT_BVH_DEVICE = 2 };
 int rt_set_bvh_builder(int mode);
 

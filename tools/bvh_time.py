@@ -1,4 +1,5 @@
-"""Host BVH8 build time (rt_bvh_export = build_bvh8 + a copy of its export):
+"""BVH8 build time (rt_bvh_export = the build + a copy of its export) with the
+host builder and, when a GPU is visible, the device builder (rt_set_bvh_builder):
 bunny and the 1.1M-triangle config-5 stand-in, best of 3.
 usage: OMP_NUM_THREADS=n python tools/bvh_time.py"""
 import ctypes as C
@@ -14,7 +15,8 @@ import rtamd  # noqa: E402
 from rtamd import data  # noqa: E402
 
 
-def build_ms(v, i):
+def build_ms(v, i, mode=1):
+    rtamd._lib.check(rtamd.lib().rt_set_bvh_builder(mode))
     v = np.ascontiguousarray(v, np.float32)
     i = np.ascontiguousarray(i, np.uint32)
     best, nn = 1e30, C.c_int64(0)
@@ -29,6 +31,9 @@ def build_ms(v, i):
 bunny = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
 big = rtamd.subdivide_mesh(bunny, 2)
 thr = os.environ.get("OMP_NUM_THREADS", "default")
+modes = [(1, "host")] + ([(2, "device")] if rtamd.device_count() > 0 else [])
 for name, m in (("bunny", bunny), ("bunny x16 (1.1M)", big)):
-    ms, n = build_ms(m.vPos4f, m.indices)
-    print(f"threads {thr}: {name}: {m.indices.size // 3} tris, {n} nodes, {ms:.1f} ms", flush=True)
+    for mode, label in modes:
+        ms, n = build_ms(m.vPos4f, m.indices, mode)
+        print(f"{label} builder, OMP threads {thr}: {name}: {m.indices.size // 3} tris, {n} nodes, {ms:.1f} ms",
+              flush=True)

@@ -26,6 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,7 +40,7 @@
 
 namespace {
 
-constexpr uint32_t kSerialMax = 1024;  // segments at most this long: one thread, serial introsort
+constexpr uint32_t kSerialMax = 256;  // segments at most this long: one wave, serial introsort in LDS
 constexpr int kScanT = 256, kScanI = 8, kScanBlk = kScanT * kScanI;
 
 struct Seg {
@@ -46,24 +49,30 @@ struct Seg {
   uint32_t pad;
 };
 
-// ---- libstdc++'s sort algorithms on ids compared by K[id] ------------------
-__device__ __forceinline__ bool lt(const float *K, uint32_t a, uint32_t b) { return K[a] < K[b]; }
-__device__ __forceinline__ void d_swap(uint32_t *a, uint32_t *b) {
-  const uint32_t t = *a;
+// ---- libstdc++'s sort algorithms --------------------------------------------
+// On an LDS array of (key, id) pairs compared by key: moving the pairs is
+// moving the ids std::sort moves, so the permutation is the same.
+struct KI {
+  float k;
+  uint32_t id;
+};
+__device__ __forceinline__ bool lt(const KI &a, const KI &b) { return a.k < b.k; }
+__device__ __forceinline__ void d_swap(KI *a, KI *b) {
+  const KI t = *a;
   *a = *b;
   *b = t;
 }
 // std::__insertion_sort
-__device__ void d_insertion(uint32_t *first, uint32_t *last, const float *K) {
+__device__ void d_insertion(KI *first, KI *last) {
   if (first == last) return;
-  for (uint32_t *i = first + 1; i != last; ++i) {
-    const uint32_t v = *i;
-    if (lt(K, v, *first)) {
-      for (uint32_t *j = i; j != first; --j) *j = *(j - 1);
+  for (KI *i = first + 1; i != last; ++i) {
+    const KI v = *i;
+    if (lt(v, *first)) {
+      for (KI *j = i; j != first; --j) *j = *(j - 1);
       *first = v;
     } else {  // std::__unguarded_linear_insert
-      uint32_t *l = i, *nx = i - 1;
-      while (lt(K, v, *nx)) {
+      KI *l = i, *nx = i - 1;
+      while (lt(v, *nx)) {
         *l = *nx;
         l = nx;
         --nx;
@@ -73,33 +82,40 @@ __device__ void d_insertion(uint32_t *first, uint32_t *last, const float *K) {
   }
 }
 // std::__move_median_to_first
-__device__ void d_median_to_first(uint32_t *r, uint32_t *a, uint32_t *b, uint32_t *c, const float *K) {
-  if (lt(K, *a, *b)) {
-    if (lt(K, *b, *c)) d_swap(r, b);
-    else if (lt(K, *a, *c)) d_swap(r, c);
-    else d_swap(r, a);
-  } else if (lt(K, *a, *c)) d_swap(r, a);
-  else if (lt(K, *b, *c)) d_swap(r, c);
-  else d_swap(r, b);
+template <class T, class LT>
+__device__ void d_median_to_first(T *r, T *a, T *b, T *c, LT less) {
+  auto sw = [](T *x, T *y) {
+    const T t = *x;
+    *x = *y;
+    *y = t;
+  };
+  if (less(*a, *b)) {
+    if (less(*b, *c)) sw(r, b);
+    else if (less(*a, *c)) sw(r, c);
+    else sw(r, a);
+  } else if (less(*a, *c)) sw(r, a);
+  else if (less(*b, *c)) sw(r, c);
+  else sw(r, b);
 }
 // std::__unguarded_partition
-__device__ uint32_t *d_partition(uint32_t *first, uint32_t *last, uint32_t *pivot, const float *K) {
+__device__ KI *d_partition(KI *first, KI *last, KI *pivot) {
   for (;;) {
-    while (lt(K, *first, *pivot)) ++first;
+    while (lt(*first, *pivot)) ++first;
     --last;
-    while (lt(K, *pivot, *last)) --last;
+    while (lt(*pivot, *last)) --last;
     if (!(first < last)) return first;
     d_swap(first, last);
     ++first;
   }
 }
-// std::__adjust_heap (with std::__push_heap)
-__device__ void d_adjust_heap(uint32_t *first, int64_t hole, int64_t len, uint32_t value, const float *K) {
+// std::__adjust_heap (with std::__push_heap), on elements of type T
+template <class T, class LT>
+__device__ void d_adjust_heap(T *first, int64_t hole, int64_t len, T value, LT less) {
   const int64_t top = hole;
   int64_t child = hole;
   while (child < (len - 1) / 2) {
     child = 2 * (child + 1);
-    if (lt(K, first[child], first[child - 1])) child--;
+    if (less(first[child], first[child - 1])) child--;
     first[hole] = first[child];
     hole = child;
   }
@@ -109,7 +125,7 @@ __device__ void d_adjust_heap(uint32_t *first, int64_t hole, int64_t len, uint32
     hole = child - 1;
   }
   int64_t parent = (hole - 1) / 2;
-  while (hole > top && lt(K, first[parent], value)) {
+  while (hole > top && less(first[parent], value)) {
     first[hole] = first[parent];
     hole = parent;
     parent = (hole - 1) / 2;
@@ -117,58 +133,74 @@ __device__ void d_adjust_heap(uint32_t *first, int64_t hole, int64_t len, uint32
   first[hole] = value;
 }
 // std::__partial_sort(first, last, last): std::__make_heap, then std::__sort_heap
-__device__ void d_heapsort(uint32_t *first, uint32_t *last, const float *K) {
+template <class T, class LT>
+__device__ void d_heapsort(T *first, T *last, LT less) {
   const int64_t len = last - first;
   if (len >= 2) {
     for (int64_t parent = (len - 2) / 2;; --parent) {
-      d_adjust_heap(first, parent, len, first[parent], K);
+      d_adjust_heap(first, parent, len, first[parent], less);
       if (parent == 0) break;
     }
   }
   while (last - first > 1) {  // std::__pop_heap(first, last - 1, last - 1)
     --last;
-    const uint32_t v = *last;
+    const T v = *last;
     *last = *first;
-    d_adjust_heap(first, 0, last - first, v, K);
+    d_adjust_heap(first, 0, last - first, v, less);
   }
 }
-// std::__introsort_loop, the recursion on the right part kept on a stack
-__device__ void d_introsort(uint32_t *first, uint32_t *last, int depth, const float *K) {
-  struct Fr {
-    uint32_t *f, *l;
-    int d;
-  } st[64];
+// std::__introsort_loop; the recursion on the right part on a stack in LDS
+// (one entry per level descended: at most the initial depth limit, <= 62)
+__device__ void d_introsort(KI *base, uint32_t len, int depth, uint32_t *stk) {
+  uint32_t f = 0, l = len;
   int sp = 0;
   for (;;) {
-    while (last - first > 16) {
+    while (l - f > 16) {
       if (depth == 0) {
-        d_heapsort(first, last, K);
+        d_heapsort(base + f, base + l, [](const KI &a, const KI &b) { return a.k < b.k; });
         break;
       }
       --depth;
-      uint32_t *mid = first + (last - first) / 2;
-      d_median_to_first(first, first + 1, mid, last - 1, K);
-      uint32_t *cut = d_partition(first + 1, last, first, K);
-      st[sp++] = Fr{cut, last, depth};
-      last = cut;
+      KI *first = base + f, *last = base + l;
+      KI *mid = first + (last - first) / 2;
+      d_median_to_first(first, first + 1, mid, last - 1, [](const KI &a, const KI &b) { return a.k < b.k; });
+      const uint32_t cut = (uint32_t)(d_partition(first + 1, last, first) - base);
+      stk[sp++] = (cut << 16) | l;  // positions < 2^16 (kSerialMax)
+      stk[sp++] = (uint32_t)depth;
+      l = cut;
     }
     if (sp == 0) break;
-    --sp;
-    first = st[sp].f;
-    last = st[sp].l;
-    depth = st[sp].d;
+    depth = (int)stk[--sp];
+    const uint32_t w = stk[--sp];
+    f = w >> 16;
+    l = w & 0xFFFFu;
   }
 }
 
-// one thread per short segment: the rest of the introsort and the final insertion sort
-__global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t cnt, uint32_t *ids, const float *K3,
-                                                uint32_t n) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= cnt) return;
-  const Seg s = segs[i];
+// one wave per short segment (<= kSerialMax): (key, id) pairs staged in LDS,
+// the rest of the introsort and the final insertion sort by lane 0
+__global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t *ids, const float *K3, uint32_t n) {
+  __shared__ KI a[kSerialMax];
+  __shared__ uint32_t stk[2 * 64];
+  const Seg s = segs[blockIdx.x];
   const float *K = K3 + (size_t)(s.first / n) * n;
-  d_introsort(ids + s.first, ids + s.last, s.depth, K);
-  d_insertion(ids + s.first, ids + s.last, K);
+  const uint32_t len = s.last - s.first;
+  if (len > kSerialMax) {  // a long segment whose depth ran out (k_prep): heapsort in place
+    if (threadIdx.x == 0)
+      d_heapsort(ids + s.first, ids + s.last, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
+    return;  // sorted: the final insertion sort leaves it unchanged
+  }
+  for (uint32_t i = threadIdx.x; i < len; i += 64) {
+    const uint32_t id = ids[s.first + i];
+    a[i] = KI{K[id], id};
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d_introsort(a, len, s.depth, stk);
+    d_insertion(a, a + len);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < len; i += 64) ids[s.first + i] = a[i].id;
 }
 
 // ---- inclusive scan of u32 (three launches) --------------------------------
@@ -239,7 +271,7 @@ __global__ void k_prep(const Seg *segs, uint32_t m, uint32_t *ids, const float *
   }
   const float *K = K3 + (size_t)(s.first / n) * n;
   uint32_t *f = ids + s.first, *l = ids + s.last;
-  d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, K);
+  d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
   kp[i] = K[*f];
   size[i] = s.last - s.first;
 }
@@ -320,7 +352,9 @@ __global__ void k_swap(const Seg *segs, const uint32_t *offs, uint32_t m, const 
   const uint32_t rank = Ai[v] - (o ? Ai[o - 1] : 0u);
   if (rank > sw[i]) return;
   const uint32_t p = segs[i].first + (v - o), q = Rpos[o + rank - 1];
-  d_swap(ids + p, ids + q);
+  const uint32_t t = ids[p];
+  ids[p] = ids[q];
+  ids[q] = t;
 }
 
 // the cut (where the left scan stops after the last swap) and the two parts:
@@ -373,9 +407,11 @@ __device__ __forceinline__ float tb_area(const TBox &b) {  // surfaceArea (raytr
   return 2 * (dx * dy + dx * dz + dy * dz);
 }
 
-constexpr int kSahT = 256;
-// inclusive scan of box unions over the block; dir = +1: thread order, -1: reverse
-__device__ TBox block_scan_box(TBox b, TBox *sm) {
+constexpr int kSahT = 256, kSahI = 8, kSahChunk = kSahT * kSahI;
+// exclusive scan of box unions over the block in thread order (earlier threads
+// first, so among equal bounds the earlier operand is kept); returns the
+// union of the threads before this one, *tot the union of all
+__device__ TBox block_excl_box(const TBox &b, TBox *sm, TBox *tot) {
   sm[threadIdx.x] = b;
   __syncthreads();
   for (int o = 1; o < kSahT; o <<= 1) {
@@ -385,13 +421,21 @@ __device__ TBox block_scan_box(TBox b, TBox *sm) {
     sm[threadIdx.x] = tb_union(x, sm[threadIdx.x]);
     __syncthreads();
   }
-  return sm[threadIdx.x];
+  const TBox ex = threadIdx.x ? sm[threadIdx.x - 1] : tb_empty();
+  *tot = sm[kSahT - 1];
+  __syncthreads();
+  return ex;
 }
 
 struct Task {
   uint32_t s, e;  // triangle range [s, e) of one candidate
 };
 
+// The sweeps of tryDivide(indices, start, end, axis) on the sorted range:
+// each thread takes kSahI consecutive triangles of a chunk, accumulated in the
+// order the reference accumulates them (the right boxes from the end, the
+// left boxes from the start), then a block scan over the threads and the
+// carry of the previous chunks; every union keeps the earlier operand.
 __global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t *ids3, const TBox *tbox, uint32_t n,
                                                TBox *rightB3, float *out_cost, uint32_t *out_div) {
   __shared__ TBox sm[kSahT];
@@ -404,13 +448,22 @@ __global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t
   TBox *rightB = rightB3 + base;
   // right boxes: union over [t, e), built from the end (triangles_raytracing.cpp:67-80)
   TBox carry = tb_empty();
-  for (int64_t hi = tk.e; hi > (int64_t)tk.s; hi -= kSahT) {
-    const int64_t t = hi - 1 - (int64_t)threadIdx.x;
-    const TBox b = (t >= (int64_t)tk.s) ? tbox[ids[t]] : tb_empty();
-    const TBox r = tb_union(carry, block_scan_box(b, sm));
-    if (t >= (int64_t)tk.s) rightB[t] = r;
-    const TBox tot = sm[kSahT - 1];
-    __syncthreads();
+  for (int64_t hi = tk.e; hi > (int64_t)tk.s; hi -= kSahChunk) {
+    TBox loc = tb_empty(), tot;
+    const int64_t t0 = hi - 1 - (int64_t)threadIdx.x * kSahI;  // this thread: t0, t0 - 1, ...
+#pragma unroll
+    for (int q = 0; q < kSahI; ++q)
+      if (t0 - q >= (int64_t)tk.s) loc = tb_union(loc, tbox[ids[t0 - q]]);
+    const TBox pre = tb_union(carry, block_excl_box(loc, sm, &tot));
+    TBox r = pre;
+#pragma unroll
+    for (int q = 0; q < kSahI; ++q) {
+      const int64_t t = t0 - q;
+      if (t >= (int64_t)tk.s) {
+        r = tb_union(r, tbox[ids[t]]);
+        rightB[t] = r;
+      }
+    }
     carry = tb_union(carry, tot);
   }
   __syncthreads();
@@ -421,22 +474,27 @@ __global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t
   float best = __builtin_huge_valf();
   uint32_t bdiv = 0xFFFFFFFFu;
   carry = tb_empty();
-  for (uint32_t lo = tk.s; lo < tk.e; lo += kSahT) {
-    const uint32_t t = lo + threadIdx.x;
-    const TBox b = (t < tk.e) ? tbox[ids[t]] : tb_empty();
-    const TBox left = tb_union(carry, block_scan_box(b, sm));
-    const TBox tot = sm[kSahT - 1];
-    const uint32_t d = t + 1;  // divider after triangle t (index units: 3 d)
-    if (d < tk.e) {
-      const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
-      const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
-      const float c = 0.2f + tb_area(left) / psa * lc + tb_area(rightB[d]) / psa * rc;
-      if (c < best) {  // NaN never wins, as `curSAH < result.sah`
-        best = c;
-        bdiv = d;
+  for (uint32_t lo = tk.s; lo < tk.e; lo += kSahChunk) {
+    TBox loc = tb_empty(), tot;
+    const uint32_t t0 = lo + threadIdx.x * kSahI;
+#pragma unroll
+    for (int q = 0; q < kSahI; ++q)
+      if (t0 + q < tk.e) loc = tb_union(loc, tbox[ids[t0 + q]]);
+    TBox left = tb_union(carry, block_excl_box(loc, sm, &tot));
+#pragma unroll
+    for (int q = 0; q < kSahI; ++q) {
+      const uint32_t t = t0 + q, d = t + 1;  // divider after triangle t (index units: 3 d)
+      if (t < tk.e) left = tb_union(left, tbox[ids[t]]);
+      if (d < tk.e) {
+        const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
+        const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
+        const float c = 0.2f + tb_area(left) / psa * lc + tb_area(rightB[d]) / psa * rc;
+        if (c < best) {  // NaN never wins, as `curSAH < result.sah`; a thread's dividers ascend
+          best = c;
+          bdiv = d;
+        }
       }
     }
-    __syncthreads();
     carry = tb_union(carry, tot);
   }
   s_cost[threadIdx.x] = best;
@@ -517,6 +575,27 @@ __global__ __launch_bounds__(kSahT) void k_range_box(const Task *ranges, const u
 }
 
 // ---- host side ---------------------------------------------------------------
+// RTAMD_BVH_TIMING=1: per-phase wall time of a device build on stderr (the
+// phases are synchronised for the measurement)
+struct PhaseTimer {
+  bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
+  double acc[8] = {};
+  int rounds = 0, stages = 0, serial_launches = 0;
+  std::chrono::steady_clock::time_point t0;
+  hipStream_t st = nullptr;
+  void start() {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    t0 = std::chrono::steady_clock::now();
+  }
+  void stop(int k) {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    acc[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+};
+PhaseTimer g_pt;
+
 template <class T>
 struct DBuf {
   T *p = nullptr;
@@ -587,7 +666,9 @@ struct Sorter {
     uint32_t hc[3] = {0, 0, nser};  // next count, next E, serial count
     HIP_TRY(hipMemcpyAsync(ctr.p + 2, &hc[2], 4, hipMemcpyHostToDevice, st));
     Seg *cur = segA.p, *nxt = segB.p;
+    g_pt.start();
     while (m > 0) {
+      ++g_pt.rounds;
       HIP_TRY(hipMemsetAsync(ctr.p, 0, 8, st));
       HIP_TRY(hipMemsetAsync(sw.p, 0, (size_t)m * 4, st));
       const uint32_t gm = (m + 255) / 256;
@@ -614,8 +695,12 @@ struct Sorter {
     }
     HIP_TRY(hipMemcpyAsync(&nser, ctr.p + 2, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (nser) k_serial<<<(nser + 63) / 64, 64, 0, st>>>(serial.p, nser, ids, K3, n);
+    g_pt.stop(0);
+    g_pt.start();
+    if (nser) k_serial<<<nser, 64, 0, st>>>(serial.p, ids, K3, n);
+    ++g_pt.serial_launches;
     HIP_TRY(hipGetLastError());
+    g_pt.stop(1);
     return RT_OK;
   }
 };
@@ -634,7 +719,7 @@ struct Open {
 namespace rth {
 
 bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                    std::string &err) {
+                    std::string &err, bool with_canon) {
   auto fail = [&](const char *what) {
     err = std::string("GPU BVH build: ") + what + ": " + rterr::get();
     return false;
@@ -647,6 +732,8 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   out = BVHGpu();
   if (n == 0) { out.root_word = rtl::kInvalidChild; return true; }
 
+  const auto tb0 = std::chrono::steady_clock::now();
+  g_pt = PhaseTimer();
   DBuf<float4> dv;
   DBuf<uint32_t> didx, ids3, backup, ddiv, dact;
   DBuf<float> K3, dcost;
@@ -662,6 +749,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return false; }
   S.st = st;
+  g_pt.st = st;
   struct StreamGuard {
     hipStream_t s;
     ~StreamGuard() { (void)hipStreamDestroy(s); }
@@ -681,7 +769,10 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   open.push_back(Open{0, 0, 3 * n, {{0u, 3 * n}}, {}, 0});
   std::vector<Task> ranges;   // child ranges (triangle units) for the final boxes
   std::vector<std::pair<int32_t, int>> range_of;  // (node, child slot) per range
+  g_pt.start();
+  g_pt.stop(7);  // allocation + upload
   while (!open.empty()) {
+    ++g_pt.stages;
     // this stage: every queued candidate of every open node that tryDivide sorts (> 8 triangles)
     std::vector<Task> tasks;
     std::vector<std::vector<int>> task_of(open.size());
@@ -708,7 +799,9 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
         for (const Task &tk : tasks)
           segs.push_back(Seg{a * n + tk.s, a * n + tk.e, 2 * lg2(tk.e - tk.s), 0});
       if (S.sort(segs)) return fail("sort");
+      g_pt.start();
       k_sah<<<3 * T, kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, n, rightB3.p, dcost.p, ddiv.p);
+      g_pt.stop(2);
       if (hipGetLastError() != hipSuccess ||
           hipMemcpyAsync(cost.data(), dcost.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipMemcpyAsync(dvd.data(), ddiv.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -831,7 +924,16 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     err = "download";
     return false;
   }
-  bvh_layout(vpos4, idx, nidx, H, cur, out);
+  g_pt.start();
+  bvh_layout(vpos4, idx, nidx, H, cur, out, with_canon);
+  g_pt.stop(3);
+  if (g_pt.on)
+    std::fprintf(stderr,
+                 "[bvh gpu] %u tris: total %.1f ms | alloc+upload %.1f, partition rounds %.1f (%d rounds), serial "
+                 "sorts %.1f (%d launches), SAH %.1f, layout %.1f; %d stages\n",
+                 n, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(),
+                 g_pt.acc[7], g_pt.acc[0], g_pt.rounds, g_pt.acc[1], g_pt.serial_launches, g_pt.acc[2], g_pt.acc[3],
+                 g_pt.stages);
   return true;
 }
 

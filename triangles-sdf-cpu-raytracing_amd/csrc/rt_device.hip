@@ -1371,20 +1371,21 @@ void launch_rays_t(const S &sc, const PlaneDev &pl, const float *o, const float 
 namespace {
 // BVH8 builder selection (rt_set_bvh_builder): both builders give the same tree
 int g_bvh_mode = RT_BVH_AUTO;
-constexpr int64_t kBvhDeviceMinTris = 131072;  // auto: the device builder from this many triangles
+constexpr int64_t kBvhDeviceMinTris = 32768;  // auto: the device builder from this many triangles
 
-int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, rth::BVHGpu &b) {
+int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, rth::BVHGpu &b,
+              bool with_canon) {
   std::string err;
   int ndev = 0;
   const bool dev = g_bvh_mode == RT_BVH_DEVICE ||
                    (g_bvh_mode == RT_BVH_AUTO && nidx / 3 >= kBvhDeviceMinTris &&
                     hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0);
   if (dev) {
-    if (!rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err))
+    if (!rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err, with_canon))
       return set_err(err.rfind("GPU BVH build", 0) == 0 ? RT_E_DEVICE : RT_E_INVALID, err);
     return RT_OK;
   }
-  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err)) return set_err(RT_E_INVALID, err);
+  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err, with_canon)) return set_err(RT_E_INVALID, err);
   return RT_OK;
 }
 
@@ -1499,8 +1500,8 @@ int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64
                   uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth) {
   if (!vpos4 || !idx || !nnodes || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "bad mesh");
   rth::BVHGpu b;
-  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b)) return rc;
-  const int64_t n = (int64_t)b.canon.size() / 52;
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, canon != nullptr)) return rc;
+  const int64_t n = canon ? (int64_t)b.canon.size() / 52 : b.host_nodes;
   if (canon) {
     if (*nnodes < n) return set_err(RT_E_INVALID, "buffer too small");
     std::memcpy(canon, b.canon.data(), b.canon.size() * 4);
@@ -1515,7 +1516,7 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
                          rt_scene **out) {
   if (!vpos4 || !idx || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "empty mesh");
   rth::BVHGpu b;
-  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b)) return rc;
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, false)) return rc;
   int32_t maxd = 8;
   int rc = pick_maxd(b.max_depth, maxd);
   if (rc) return rc;

@@ -476,7 +476,7 @@ struct Builder {
 }  // namespace
 
 bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                std::string &err) {
+                std::string &err, bool with_canon) {
   if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
   const size_t ntri = (size_t)nidx / 3;
   for (int64_t i = 0; i < nidx; ++i)
@@ -513,19 +513,20 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     B.create(0, 0, (size_t)nidx);
   }
 
-  bvh_layout(vpos4, idx, nidx, B.nodes, B.cur, out);
+  bvh_layout(vpos4, idx, nidx, B.nodes, B.cur, out, with_canon);
   return true;
 }
 
 void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
-                const std::vector<uint32_t> &cur, BVHGpu &out) {
-  const size_t ntri = (size_t)nidx / 3;
+                const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon) {
+  const int64_t ntri = nidx / 3;
   out.host_nodes = (int64_t)H.size();
   out.perm_tri = cur;
   out.perm_idx.resize((size_t)nidx);
-  for (size_t t = 0; t < ntri; ++t)
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < ntri; ++t)
     for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)cur[t] + k];
-  {  // canonical pre-order (52 u32 per node), same as the oracle's export
+  if (with_canon) {  // canonical pre-order (52 u32 per node), same as the oracle's export
     std::vector<int32_t> st{0};
     while (!st.empty()) {
       int32_t id = st.back();
@@ -553,32 +554,45 @@ void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std
     }
   }
 
+  // leaves take consecutive triangle slots in the order they are met; the
+  // slots are filled afterwards, in parallel
+  std::vector<std::pair<uint32_t, uint32_t>> leaf_fill;  // (first slot, leaf's first triangle position)
+  std::vector<uint32_t> leaf_cnt;
+  uint32_t next_slot = 0;
   auto leaf_word = [&](const HNode &n) -> uint32_t {
-    const uint32_t first = (uint32_t)out.tris.size();
-    const uint32_t nt = n.count / 3;
-    for (uint32_t k = 0; k < nt; ++k) {
-      const uint32_t slot = n.start / 3 + k;
-      const uint32_t *tv = idx + 3 * (size_t)cur[slot];
-      float v[3][3];
-      for (int j = 0; j < 3; ++j) {
-        const float *p = vpos4 + 4 * (size_t)tv[j];
-        const float w = p[3];
-        v[j][0] = p[0] / w; v[j][1] = p[1] / w; v[j][2] = p[2] / w;  // v /= v.w (:307-309)
-      }
-      rtl::GTri g;
-      g.v0x = v[0][0]; g.v0y = v[0][1]; g.v0z = v[0][2];
-      g.orig_id = cur[slot];
-      g.e1x = v[1][0] - v[0][0]; g.e1y = v[1][1] - v[0][1]; g.e1z = v[1][2] - v[0][2];
-      g.e2x = v[2][0] - v[0][0]; g.e2y = v[2][1] - v[0][1]; g.e2z = v[2][2] - v[0][2];
-      g.pad1 = g.pad2 = 0.0f;
-      out.tris.push_back(g);
-    }
+    const uint32_t first = next_slot, nt = n.count / 3;
     if (nt == 0) return rtl::kInvalidChild;
+    next_slot += nt;
+    leaf_fill.push_back({first, n.start / 3});
+    leaf_cnt.push_back(nt);
     return rtl::kLeafBit | (first << 3) | (nt - 1);
+  };
+  auto fill_tris = [&]() {
+    out.tris.resize(next_slot);
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t l = 0; l < (int64_t)leaf_fill.size(); ++l) {
+      for (uint32_t k = 0; k < leaf_cnt[l]; ++k) {
+        const uint32_t slot = leaf_fill[l].second + k;
+        const uint32_t *tv = idx + 3 * (size_t)cur[slot];
+        float v[3][3];
+        for (int j = 0; j < 3; ++j) {
+          const float *p = vpos4 + 4 * (size_t)tv[j];
+          const float w = p[3];
+          v[j][0] = p[0] / w; v[j][1] = p[1] / w; v[j][2] = p[2] / w;  // v /= v.w (:307-309)
+        }
+        rtl::GTri &g = out.tris[leaf_fill[l].first + k];
+        g.v0x = v[0][0]; g.v0y = v[0][1]; g.v0z = v[0][2];
+        g.orig_id = cur[slot];
+        g.e1x = v[1][0] - v[0][0]; g.e1y = v[1][1] - v[0][1]; g.e1z = v[1][2] - v[0][2];
+        g.e2x = v[2][0] - v[0][0]; g.e2y = v[2][1] - v[0][1]; g.e2z = v[2][2] - v[0][2];
+        g.pad1 = g.pad2 = 0.0f;
+      }
+    }
   };
 
   if (H[0].leaf) {
     out.root_word = leaf_word(H[0]);
+    fill_tris();
     out.max_depth = 0;
     out.host_inner = 0;
     return;
@@ -623,6 +637,7 @@ void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std
     for (uint32_t c = 0; c < r.nchild; ++c) grow(u, r.box[c]);
     for (int k = 0; k < 3; ++k) { out.root_box[k] = u.mn[k]; out.root_box[3 + k] = u.mx[k]; }
   }
+  fill_tris();
 }
 
 // --------------------------------------------------------------- octree ---

@@ -33,8 +33,9 @@ struct BVHGpu {
   std::vector<uint32_t> perm_idx;  // mesh indices after the build's permutation
   std::vector<uint32_t> perm_tri;  // original triangle id per triangle slot
 };
+// with_canon: also fill BVHGpu::canon (rt_bvh_export; scene creation skips it)
 bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                std::string &err);
+                std::string &err, bool with_canon = true);
 
 // The tree BVHBuilder::perform builds (triangles_raytracing.cpp:155-225), as
 // either builder produces it: nodes (node 0 = root; children anywhere) and the
@@ -53,12 +54,12 @@ struct BvhHostNode {
 void host_introsort(uint32_t *ids, size_t n, const float *K, int64_t depth_limit);
 // Canonical export + GPU layout (GNode / GTri, BFS over inner nodes) of a built tree.
 void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
-                const std::vector<uint32_t> &cur, BVHGpu &out);
+                const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon = true);
 // The same tree built on the current HIP device (rt_bvhgpu.hip): libstdc++'s
 // introsort replicated with parallel Hoare partitions, SAH sweeps as device
 // scans. Identical output to build_bvh8.
 bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                    std::string &err);
+                    std::string &err, bool with_canon = true);
 
 struct OctGpu {
   std::vector<rtl::OctWord> child;    // per node: {0 leaf, kOctNeverHits or childrenOffset; child masks}
