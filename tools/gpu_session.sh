@@ -1,7 +1,17 @@
 #!/bin/bash
-# One gpurun session: GPU tests, the driver's bench command, a long bench run and a
-# rocprofv3 kernel-stats pass. usage (on the box): tools/gpu_session.sh OUT [steps...]
-#   steps: tests | fulltests | bench | bench128 | prof | split
+# One gpurun session: GPU tests, the driver's bench command, a long bench run,
+# a rocprofv3 kernel-stats pass and A/B legs. usage (on the box):
+#   tools/gpu_session.sh OUT step [step ...]
+# steps:
+#   tests | fulltests | smoke | bench | bench128 | prof | split | dist_gloo | dist_rccl1
+#   ab=VAR=a,VAR2=b    tools/ab.py batch on $AB_WL (default bunny) under those
+#                      settings (RTAMD_LIB=<lib/var_x.so> selects a build variant,
+#                      AB_VARIANTS the frames x streams); ab= alone: no settings
+#   short=VAR=a,...    bench.py at 20 and 128 steps (headline only) under them
+#   tail=VAR=a,...     tools/persist_tail.py on $AB_WL (needs the stamps variant:
+#                      bash tools/build_variant.sh stamps -DRT_PERSIST_STAMPS)
+#   pmc=VAR=a,...      rocprofv3 --pmc $PMC_COUNTERS over tools/prof_frames.py
+#                      --plan $PMC_PLAN (one counter pass; see bench.PMC_PASSES)
 # Every GPU step runs under its own timeout; the first failure ends the session.
 set -o pipefail
 OUT=${1:-gpurun_out/s}; shift
@@ -10,7 +20,12 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 run() { local name=$1 secs=$2; shift 2
   echo "== $name: $*"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
   echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"; return $rc; }
+n=0
 for step in "$@"; do
+  n=$((n + 1))
+  arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
+  envs=(${arg//,/ })
+  tag="$n.${step%%=*}"
   case $step in
     tests) run tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not fullsize" || exit 1 ;;
     fulltests) run fulltests 600 python -u -m pytest tests/test_fullsize.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
@@ -21,6 +36,15 @@ for step in "$@"; do
     split) run split 600 python tools/ab.py split bunny || exit 1 ;;
     dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && tail -1 "$OUT/dist_gloo.log" > "$OUT/dist_gloo.json" || exit 1 ;;
     dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && tail -1 "$OUT/dist_rccl1.log" > "$OUT/dist_rccl1.json" || exit 1 ;;
+    ab=*) echo "== $tag [$arg]"; run "$tag" 300 env "${envs[@]}" python tools/ab.py batch ${AB_WL:-bunny} || exit 1
+          grep -v amdgpu "$OUT/$tag.log" ;;
+    short=*) for st in 20 128; do
+               run "$tag.$st" 300 env "${envs[@]}" python bench.py --steps $st --warmup 5 --no-pmc --no-cpu-baseline --no-extra || exit 1
+               python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('[$arg] bench steps', sys.argv[2], d['ms_per_step'], 'ms/frame')" "$OUT/$tag.$st.log" $st
+             done ;;
+    tail=*) run "$tag" 300 env "${envs[@]}" python tools/persist_tail.py ${AB_WL:-bunny} || exit 1
+            grep -v amdgpu "$OUT/$tag.log" ;;
+    pmc=*) run "$tag" 120 env "${envs[@]}" rocprofv3 --pmc $PMC_COUNTERS --output-format csv -d "$OUT/$tag" -o p -- python3 tools/prof_frames.py --plan "$PMC_PLAN" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

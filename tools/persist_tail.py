@@ -31,9 +31,17 @@ L.rtx_set_persist_stamps.argtypes = [C.c_void_p, C.c_int64]
 CAP = 1 << 16
 
 
+def where(item, n, W, H, g=2):
+    """frame and pixel origin of a queue item of G = 2 tiles (16 x 8 pixels)"""
+    tx = -(-W // (8 * g))
+    per = tx * -(-H // 8)
+    f, r = divmod(int(item), per)
+    return f"frame {f} x {(r % tx) * 8 * g} y {(r // tx) * 8}"
+
+
 def main():
     names = sys.argv[1:] or ["bunny"]
-    buf = torch.zeros(CAP * 4, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(CAP * 8, dtype=torch.int64, device="cuda")
     for name in names:
         src, W, H, mode, _ = bench.WORKLOADS[name]
         sc, off = WL.scene_for(src)
@@ -49,7 +57,7 @@ def main():
             rtamd._lib.check(L.rtx_set_persist_stamps(C.c_void_p(buf.data_ptr()), CAP))
             bench.run_single(sc, prm, 0, n, W, H, inflight=1, batch=n)
             rtamd._lib.check(L.rtx_set_persist_stamps(None, 0))
-            s = buf.view(-1, 4).cpu().numpy()
+            s = buf.view(-1, 8).cpu().numpy()
             s = s[s[:, 1] > 0]
             t0 = s[:, 0].min()
             st, en = (s[:, 0] - t0) / 100.0, (s[:, 1] - t0) / 100.0  # us (100 MHz)
@@ -62,6 +70,18 @@ def main():
                   f"{np.median(en):.1f}/{np.percentile(en, 90):.1f} us, tail (last end - first out) "
                   f"{en.max() - drained:.1f} us, items/wave mean {items.mean():.1f} max {items.max()}, "
                   f"exit probe after last item max {(en - last_item).max():.1f} us", flush=True)
+            # the waves that end last: their last item (start, duration) and
+            # the longest items of the launch
+            dur = (s[:, 3] - s[:, 4]) / 100.0
+            lstart = (s[:, 4] - t0) / 100.0
+            for w in np.argsort(-en)[:4]:
+                print(f"    late wave: ends {en[w]:.1f} us, last item {s[w, 5]} ({where(s[w, 5], n, W, H)}) "
+                      f"started {lstart[w]:.1f} us, ran {dur[w]:.1f} us", flush=True)
+            dmax = s[:, 6] / 100.0
+            for w in np.argsort(-dmax)[:4]:
+                print(f"    longest item: {s[w, 7]} ({where(s[w, 7], n, W, H)}) {dmax[w]:.1f} us", flush=True)
+            print(f"    item duration over waves' longest: p50 {np.median(dmax):.1f} us, p99 "
+                  f"{np.percentile(dmax, 99):.1f} us", flush=True)
         a = np.polyfit([n for n, _ in fits], [k for _, k in fits], 1)
         print(f"{name}: launch ms ~= {a[1]:.4f} + {a[0]:.4f} * frames", flush=True)
         sc.close()

@@ -477,8 +477,9 @@ struct PersistQ {
   uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
   uint32_t stride;   // words between heads
   // diagnostic builds (-DRT_PERSIST_STAMPS, tools/build_variant.sh; see
-  // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 4 x u64 =
-  // start, end (s_memrealtime, 100 MHz), items traced, end of its last item
+  // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 8 x u64 =
+  // start, end (s_memrealtime, 100 MHz), items traced | XCD << 32, end of its
+  // last item, start of its last item, last item, longest item's duration, longest item
   unsigned long long *stamps;
 };
 // 4 KiB + 256 B apart: every head on its own memory channel's lines, so the
@@ -501,8 +502,8 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
   const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
 #ifdef RT_PERSIST_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  unsigned long long t_item = t_start;
-  uint32_t n_items = 0;
+  unsigned long long t_item = t_start, t_last = t_start, d_max = 0;
+  uint32_t n_items = 0, last_item = 0, max_item = 0;
 #endif
   uint32_t h = xcc;
   uint32_t k = q_claim(q.heads + h * q.stride);
@@ -526,23 +527,44 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
     const uint32_t knext = q_claim(q.heads + h * q.stride);
     const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
+#ifdef RT_PERSIST_STAMPS
+    const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+#endif
     for (uint32_t j = 0; j < q.gy; ++j)
-      for (uint32_t i = 0; i < q.gx; ++i)
-        render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[f], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
+      for (uint32_t i = 0; i < q.gx; ++i) {
+        // the frame index is made opaque per tile, so the frame's arguments
+        // (two 4x4 matrices among them) are re-read from the kernarg segment by
+        // each tile instead of being hoisted out of the tile loop and kept
+        // live across the traversal
+        uint32_t fo = f;
+        asm volatile("" : "+s"(fo));
+        render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[fo], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
                                             (int)((ty * q.gy + j) * 8) + (lane >> 3));
+      }
 #ifdef RT_PERSIST_STAMPS
     ++n_items;
     t_item = __builtin_amdgcn_s_memrealtime();
+    t_last = t_begin;
+    last_item = item;
+    if (t_item - t_begin > d_max) {
+      d_max = t_item - t_begin;
+      max_item = item;
+    }
 #endif
     k = knext;
   }
 #ifdef RT_PERSIST_STAMPS
   if (q.stamps && lane == 0) {
     const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    q.stamps[4 * w] = t_start;
-    q.stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
-    q.stamps[4 * w + 2] = n_items | ((unsigned long long)xcc << 32);
-    q.stamps[4 * w + 3] = t_item;
+    unsigned long long *o = q.stamps + 8 * w;
+    o[0] = t_start;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+    o[2] = n_items | ((unsigned long long)xcc << 32);
+    o[3] = t_item;
+    o[4] = t_last;
+    o[5] = last_item;
+    o[6] = d_max;
+    o[7] = max_item;
   }
 #endif
   if (lane == 0) {
@@ -2017,7 +2039,7 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 }
 
 // Diagnostic: persistent launches from now on write per-wave stamps (see
-// PersistQ::stamps) into the device buffer d_buf of cap_waves x 4 u64
+// PersistQ::stamps) into the device buffer d_buf of cap_waves x 8 u64
 // (d_buf = NULL turns it off). Not part of include/rtamd.h.
 int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
   g_persist_stamps = (unsigned long long *)d_buf;
