@@ -121,6 +121,48 @@ def test_intersect_rays(gpu, name, plane, tn, tf):
     assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
 
 
+def _centre_plane_rays(seed):
+    """Rays between dyadic points (exact in float32, d unnormalised): aimed at
+    octree box corners, centres, edge and face midpoints at depths 0-6, from
+    dyadic origins, many of them on centre planes. Their centre-plane
+    distances tie (a ray through a centre edge or point) or tie with the entry,
+    the cases where oct_expand must take the exact slab + sort8 path."""
+    rng = np.random.default_rng(seed)
+    n = 20000
+    depth = rng.integers(0, 7, n)
+    s = np.ldexp(2.0, -depth)                       # node size 2^(1-k)
+    cells = np.ldexp(1.0, depth).astype(np.int64)    # 2^k cells per axis
+    idx = rng.integers(0, cells[:, None], (n, 3))
+    frac = rng.choice([0.0, 0.5, 1.0], (n, 3), p=[0.25, 0.5, 0.25])
+    tgt = -1.0 + (idx + frac) * s[:, None]
+    o = rng.choice(np.arange(-12, 13) / 4.0, (n, 3))
+    far = rng.random(n) < 0.7                        # most origins outside the [-1, 1] box
+    o[far] = o[far] * 2.0 + np.sign(o[far] + 0.125) * 1.5
+    d = tgt - o
+    d[np.all(d == 0, axis=1)] = (0.25, -0.5, 1.0)
+    return o.astype(np.float32), d.astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["sdf_5.octree", "sdf_6.octree"])
+@pytest.mark.parametrize("tn,tf", [(0.01, 100.0), (-5.0, 100.0)])
+def test_octree_centre_plane_rays(gpu, name, tn, tf):
+    """SDFOctree::intersect on rays whose slab distances tie at node centres
+    (crossing-order path vs sort8 fallback in oct_expand): hit, t, normal and
+    node id exact."""
+    o, d = _centre_plane_rays(zlib.crc32(f"{name}{tn}".encode()))
+    rs, gs = S.ref_scene(name), S.gpu_scene(name)
+    rs.set_plane(False, (0, 1, 0), 0.0)
+    gs.set_plane(None)
+    rh, rt_, rn, rp = rs.intersect_rays(o, d, tn, tf)
+    g = gs.intersect(o, d, tn, tf)
+    assert rh.sum() > 1000, "too few hits to be a test"
+    assert np.array_equal(rh.astype(bool), g.hitten), "hit mask differs"
+    assert np.array_equal(rp, g.prim), "node ids differ"
+    h = g.hitten
+    assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
+    assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
+
+
 @pytest.mark.parametrize("nranks,band", [(2, 16), (3, 7), (8, 16), (5, 1000)])
 def test_row_band_tiles(gpu, nranks, band):
     """Row-band tiling (multi-GPU split): every rank's packed bands, untiled on the

@@ -980,48 +980,124 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   return false;
 }
 
+// the entries of a sorted child list (oct_expand) whose bit is set in keep
+__device__ __forceinline__ void oct_filter(uint32_t &list, uint32_t &cnt, uint32_t keep) {
+  uint32_t out = 0, n = 0, l = list;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t id = l & 7u;
+    if ((uint32_t)i < cnt && ((keep >> id) & 1u)) {
+      out |= id << (3 * n);
+      ++n;
+    }
+    l >>= 3;
+  }
+  list = out;
+  cnt = n;
+}
+
+// 1: oct_expand takes the crossing-order path when it provably gives sort8's
+// list (A/B switch; 0 always runs the 8-child slab test and sort8)
+#ifndef RT_OCT_PATH
+#define RT_OCT_PATH 1
+#endif
+
 // Expand an octree inner node: divide_box_8 + intersect_box_8 + sort8, keep
-// entries with t > 0 (octree_raytracing.cpp:175-199). The 8 child boxes have
-// only 3 distinct bounds per axis (min, centre, max: centre + diff == max and
-// min + diff == centre exactly), so the 24 slab distances of the reference
-// are 9 distinct values, computed once each with the reference's operations.
+// entries with t > 0 (octree_raytracing.cpp:175-199), then only the children
+// whose bit is set in `keep` (the child masks; 0xFF keeps all). The 8 child
+// boxes have only 3 distinct bounds per axis (min, centre, max: centre + diff
+// == max and min + diff == centre exactly), so the 24 slab distances of the
+// reference are 9 distinct values, computed once each with the reference's
+// operations.
+//
+// Crossing-order path (FAST, i.e. 1/d finite). Per axis the ray's interval in
+// the half it meets first ("near") is [entry, s] and in the other [s, exit],
+// s = the centre-plane distance, so a child's reference values are
+//   tMin = max(P, s_a over its far axes), tMax = min(Q, s_a over its near axes)
+// with P = max(the 3 entries, tNear), Q = min(the 3 exits, tFar) -- the same
+// floats the reference's max/min chains select. With the three s strictly
+// ordered s_1 < s_2 < s_3, a child whose far axes are not a prefix of that
+// order has tMin >= s_b > s_a >= tMax for some pair, so it is never entered;
+// the candidates are the 4 children met by flipping the axes in order of s.
+// If the kept ones (t > 0) have strictly increasing t, every correct sort
+// lists them in that order, so the result equals sort8's. Equal s values or
+// equal kept t (a ray through a centre edge or entering on a centre plane)
+// take the exact slab + sort8 path.
 template <bool FAST>
 __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar,
-                                           uint32_t &list, uint32_t &cnt) {
+                                           uint32_t keep, uint32_t &list, uint32_t &cnt) {
   const f3 center{(bmin.x + bmax.x) / 2.0f, (bmin.y + bmax.y) / 2.0f, (bmin.z + bmax.z) / 2.0f};
   const f3 diff = center - bmin;
   const f3 hi{center.x + diff.x, center.y + diff.y, center.z + diff.z};  // == bmax, the child max
   const float x0 = (bmin.x - o.x) * inv.x, x1 = (center.x - o.x) * inv.x, x2 = (hi.x - o.x) * inv.x;
   const float y0 = (bmin.y - o.y) * inv.y, y1 = (center.y - o.y) * inv.y, y2 = (hi.y - o.y) * inv.y;
   const float z0 = (bmin.z - o.z) * inv.z, z1 = (center.z - o.z) * inv.z, z2 = (hi.z - o.z) * inv.z;
-  // per axis and half: (min, max) of the two slab distances, ISPC operand order
-  // FAST (1/d finite, so no NaN operand): IEEE min/max equal ISPC's forms (see slab_fast)
-  auto mn = [](float a, float b) { return FAST ? __builtin_fminf(a, b) : isp_min(a, b); };
-  auto mx = [](float a, float b) { return FAST ? __builtin_fmaxf(a, b) : isp_max(a, b); };
-  const float mnx[2] = {mn(x0, x1), mn(x1, x2)}, mxx[2] = {mx(x0, x1), mx(x1, x2)};
-  const float mny[2] = {mn(y0, y1), mn(y1, y2)}, mxy[2] = {mx(y0, y1), mx(y1, y2)};
-  const float mnz[2] = {mn(z0, z1), mn(z1, z2)}, mxz[2] = {mx(z0, z1), mx(z1, z2)};
-  float t[8];
-  uint32_t id[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int x = c >> 2, y = (c & 3) >> 1, z = c & 1;
-    float tMin = mx(mnx[x], mx(mny[y], mnz[z]));
-    float tMax = mn(mxx[x], mn(mxy[y], mxz[z]));
-    tMin = mx(tMin, tNear);
-    tMax = mn(tMax, tFar);
-    t[c] = (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
-    id[c] = (uint32_t)c;
+  bool exact = !FAST || !RT_OCT_PATH;
+  if constexpr (FAST && RT_OCT_PATH) {
+    // near half per axis: 0 when the ray runs towards +axis (1/d > 0), else 1
+    const bool px = inv.x > 0.0f, py = inv.y > 0.0f, pz = inv.z > 0.0f;
+    const float P = __builtin_fmaxf(__builtin_fmaxf(px ? x0 : x2, __builtin_fmaxf(py ? y0 : y2, pz ? z0 : z2)), tNear);
+    const float Q = __builtin_fminf(__builtin_fminf(px ? x2 : x0, __builtin_fminf(py ? y2 : y0, pz ? z2 : z0)), tFar);
+    // the centre-plane distances in ascending order, with their child-id bits
+    float s0 = x1, s1 = y1, s2 = z1;
+    uint32_t b0 = 4u, b1 = 2u, b2 = 1u;
+    auto cswap = [](float &sa, uint32_t &ba, float &sb, uint32_t &bb) {
+      const bool sw = sb < sa;
+      const float t = sa; sa = sw ? sb : sa; sb = sw ? t : sb;
+      const uint32_t u = ba; ba = sw ? bb : ba; bb = sw ? u : bb;
+    };
+    cswap(s0, b0, s1, b1);
+    cswap(s1, b1, s2, b2);
+    cswap(s0, b0, s1, b1);
+    const float k0 = P, k1 = __builtin_fmaxf(P, s0), k2 = __builtin_fmaxf(P, s1), k3 = __builtin_fmaxf(P, s2);
+    const float m0 = __builtin_fminf(Q, s0), m1 = __builtin_fminf(Q, s1), m2 = __builtin_fminf(Q, s2), m3 = Q;
+    const bool e0 = !(m0 < 0.0f || k0 > m0) && k0 > 0.0f, e1 = !(m1 < 0.0f || k1 > m1) && k1 > 0.0f;
+    const bool e2 = !(m2 < 0.0f || k2 > m2) && k2 > 0.0f, e3 = !(m3 < 0.0f || k3 > m3) && k3 > 0.0f;
+    exact = !(s0 < s1 && s1 < s2) || (e0 && e1 && !(k0 < k1)) || (e1 && e2 && !(k1 < k2)) ||
+            (e2 && e3 && !(k2 < k3));
+    const uint32_t c0 = (px ? 0u : 4u) | (py ? 0u : 2u) | (pz ? 0u : 1u);
+    const uint32_t c1 = c0 ^ b0, c2 = c1 ^ b1, c3 = c2 ^ b2;
+    // pack from the back so the first visit ends in the low bits
+    uint32_t l = 0, n = 0;
+    if (e3 && ((keep >> c3) & 1u)) { l = c3; n = 1; }
+    if (e2 && ((keep >> c2) & 1u)) { l = (l << 3) | c2; ++n; }
+    if (e1 && ((keep >> c1) & 1u)) { l = (l << 3) | c1; ++n; }
+    if (e0 && ((keep >> c0) & 1u)) { l = (l << 3) | c0; ++n; }
+    list = l;
+    cnt = n;
   }
-  sort8(t, id);
-  list = 0;
-  cnt = 0;
+  if (exact) {
+    // per axis and half: (min, max) of the two slab distances, ISPC operand order
+    // FAST (1/d finite, so no NaN operand): IEEE min/max equal ISPC's forms (see slab_fast)
+    auto mn = [](float a, float b) { return FAST ? __builtin_fminf(a, b) : isp_min(a, b); };
+    auto mx = [](float a, float b) { return FAST ? __builtin_fmaxf(a, b) : isp_max(a, b); };
+    const float mnx[2] = {mn(x0, x1), mn(x1, x2)}, mxx[2] = {mx(x0, x1), mx(x1, x2)};
+    const float mny[2] = {mn(y0, y1), mn(y1, y2)}, mxy[2] = {mx(y0, y1), mx(y1, y2)};
+    const float mnz[2] = {mn(z0, z1), mn(z1, z2)}, mxz[2] = {mx(z0, z1), mx(z1, z2)};
+    float t[8];
+    uint32_t id[8];
 #pragma unroll
-  for (int i = 7; i >= 0; --i) {
-    if (t[i] > 0.0f) {
-      list = (list << 3) | id[i];
-      cnt += 1;
+    for (int c = 0; c < 8; ++c) {
+      const int x = c >> 2, y = (c & 3) >> 1, z = c & 1;
+      float tMin = mx(mnx[x], mx(mny[y], mnz[z]));
+      float tMax = mn(mxx[x], mn(mxy[y], mxz[z]));
+      tMin = mx(tMin, tNear);
+      tMax = mn(tMax, tFar);
+      t[c] = (tMax < 0.0f || tMin > tMax) ? -1.0f : tMin;
+      id[c] = (uint32_t)c;
     }
+    sort8(t, id);
+    uint32_t l = 0, n = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      if (t[i] > 0.0f) {
+        l = (l << 3) | id[i];
+        n += 1;
+      }
+    }
+    if (keep != 0xFFu) oct_filter(l, n, keep);
+    list = l;
+    cnt = n;
   }
 }
 
@@ -1053,22 +1129,6 @@ struct OctRay {
 // ray status: still traversing (suspended), finished without a hit, with a hit
 enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 
-// the entries of a sorted child list (oct_expand) whose bit is set in keep
-__device__ __forceinline__ void oct_filter(uint32_t &list, uint32_t &cnt, uint32_t keep) {
-  uint32_t out = 0, n = 0, l = list;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t id = l & 7u;
-    if ((uint32_t)i < cnt && ((keep >> id) & 1u)) {
-      out |= id << (3 * n);
-      ++n;
-    }
-    l >>= 3;
-  }
-  list = out;
-  cnt = n;
-}
-
 // SDFOctree::intersect -> intersectNode(0) (octree_raytracing.cpp:166-208), root stage.
 template <bool NEED_NORMAL, bool FAST, class CT>
 __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
@@ -1089,8 +1149,7 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   float inv_s;
   oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
   uint32_t l, c;
-  oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
-  if (!CT::kCounts) oct_filter(l, c, rw.masks);
+  oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, CT::kCounts ? 0xFFu : (rw.masks & 0xFFu), l, c);
   R = OctRay{root, l | (c << 24), rw.masks >> 8, 0u, 0u, 0u, 0};
   return c == 0 ? RAY_MISS : RAY_PENDING;
 }
@@ -1151,8 +1210,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
       continue;
     }
     uint32_t l, c;
-    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, l, c);
-    if (MASKS) oct_filter(l, c, cw.masks);
+    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, MASKS ? (cw.masks & 0xFFu) : 0xFFu, l, c);
     if (c == 0) continue;
     st.at(depth, 0) = fbase;
     st.at(depth, 1) = flist | (fcnt << 24);
