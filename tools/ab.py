@@ -10,7 +10,8 @@ launch machinery, so numbers are comparable with the bench).
   python tools/ab.py modes [workload ...]   primary and default shading
 
 workload: a key of bench.WORKLOADS (bunny, grid, grid_shipped, octree,
-octree_shipped, mesh_large) or a shipped input file. Build variants are
+octree_shipped, mesh_large, default_mode: rendered in its own shading mode)
+or a shipped input file. Build variants are
 compared by running this under different RTAMD_LIB libraries
 (tools/build_variant.sh) or RTAMD_* switches.
 """
@@ -33,11 +34,11 @@ WARM, STEPS = 16, 128
 
 def resolve(name):
     if name in bench.WORKLOADS:
-        src, W, H, _, _ = bench.WORKLOADS[name]
+        src, W, H, mode, _ = bench.WORKLOADS[name]
     else:
-        src, W, H = name, 1920, 1080
+        src, W, H, mode = name, 1920, 1080, "primary"
     sc, off = WL.scene_for(src)
-    return sc, off, W, H
+    return sc, off, W, H, mode
 
 
 def timed(sc, prm, W, H, streams, group, tile=None):
@@ -50,15 +51,17 @@ def main():
     names = sys.argv[2:] or ["bunny"]
     rtamd.lib().rt_set_device(0)
     for name in names:
-        sc, off, W, H = resolve(name)
-        sc.set_plane(None)
-        prm = bench.orbit_params(WARM + STEPS, W, H)
+        sc, off, W, H, wmode = resolve(name)
+        sc.set_plane(None if wmode == "primary" else rtamd.Plane((0.0, 1.0, 0.0), off))
+        prm = bench.orbit_params(WARM + STEPS, W, H, wmode)
         if what == "batch":
             for v in os.environ.get("AB_VARIANTS", "8x2,8x1,4x2,1x1").split(","):
                 g, s = (int(x) for x in v.split("x"))
                 ms, kms = timed(sc, prm, W, H, s, g)
                 print(f"{name} {g} frames x {s} streams: {ms:.4f} ms/frame, {kms:.4f} ms/launch", flush=True)
         elif what == "split":
+            sc.set_plane(None)
+            prm = bench.orbit_params(WARM + STEPS, W, H)
             base, _ = timed(sc, prm, W, H, 2, 8)
             print(f"{name} N=1: {base:.4f} ms/frame", flush=True)
             for n in (int(x) for x in os.environ.get("AB_NS", "2,4,8").split(",")):

@@ -7,11 +7,14 @@
 #   ab=VAR=a,VAR2=b    tools/ab.py batch on $AB_WL (default bunny) under those
 #                      settings (RTAMD_LIB=<lib/var_x.so> selects a build variant,
 #                      AB_VARIANTS the frames x streams); ab= alone: no settings
+#   ptest=VAR=a,...    the GPU tests selected by -k "$AB_K" (default: all but
+#                      the full-size ones) under those settings
 #   short=VAR=a,...    bench.py at 20 and 128 steps (headline only) under them
 #   tail=VAR=a,...     tools/persist_tail.py on $AB_WL (needs the stamps variant:
 #                      bash tools/build_variant.sh stamps -DRT_PERSIST_STAMPS)
 #   pmc=VAR=a,...      rocprofv3 --pmc $PMC_COUNTERS over tools/prof_frames.py
-#                      --plan $PMC_PLAN (one counter pass; see bench.PMC_PASSES)
+#                      --plan $PMC_PLAN (one counter pass; see bench.PMC_PASSES);
+#                      counters may be joined by '+' (pmc=PMC_COUNTERS=A+B+C)
 # Every GPU step runs under its own timeout; the first failure ends the session.
 set -o pipefail
 OUT=${1:-gpurun_out/s}; shift
@@ -38,13 +41,15 @@ for step in "$@"; do
     dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && tail -1 "$OUT/dist_rccl1.log" > "$OUT/dist_rccl1.json" || exit 1 ;;
     ab=*) echo "== $tag [$arg]"; run "$tag" 300 env "${envs[@]}" python tools/ab.py batch ${AB_WL:-bunny} || exit 1
           grep -v amdgpu "$OUT/$tag.log" ;;
+    ptest=*) run "$tag" 600 env "${envs[@]}" python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "${AB_K:-not fullsize}" || exit 1 ;;
     short=*) for st in 20 128; do
                run "$tag.$st" 300 env "${envs[@]}" python bench.py --steps $st --warmup 5 --no-pmc --no-cpu-baseline --no-extra || exit 1
                python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('[$arg] bench steps', sys.argv[2], d['ms_per_step'], 'ms/frame')" "$OUT/$tag.$st.log" $st
              done ;;
     tail=*) run "$tag" 300 env "${envs[@]}" python tools/persist_tail.py ${AB_WL:-bunny} || exit 1
             grep -v amdgpu "$OUT/$tag.log" ;;
-    pmc=*) run "$tag" 120 env "${envs[@]}" rocprofv3 --pmc $PMC_COUNTERS --output-format csv -d "$OUT/$tag" -o p -- python3 tools/prof_frames.py --plan "$PMC_PLAN" || exit 1 ;;
+    pmc=*) for e in "${envs[@]}"; do [ "${e%%=*}" = PMC_COUNTERS ] && PMC_COUNTERS=${e#*=}; done
+           run "$tag" 120 env "${envs[@]}" rocprofv3 --pmc ${PMC_COUNTERS//+/ } --output-format csv -d "$OUT/$tag" -o p -- python3 tools/prof_frames.py --plan "$PMC_PLAN" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -63,12 +63,20 @@ struct FrameArgs {
 #ifndef RT_OCT_WAVES
 #define RT_OCT_WAVES 6
 #endif
-// mesh primary: a floor of 4 waves per SIMD (128 VGPRs; the compiler alone
-// takes 142, 3 waves). With leaf batches of 2 triangles (RT_LEAF_BATCH,
-// rt_scenes.h) it spills 36 B per lane; same-box A/B, 8 frames x 2 streams:
-// bunny 1080p 0.1191 -> 0.1157 ms/frame, 1.1M tris 4K 0.482 -> 0.457.
+// mesh primary: a floor of 4 waves per SIMD (128 VGPRs). The persistent kernel
+// fits it without scratch at leaf batches of 4 triangles (127 VGPRs,
+// RT_LEAF_BATCH_PRIMARY in rt_scenes.h; round 1 needed batches of 2 and still
+// spilled 36 B per lane); a 5-wave floor is slower.
 #ifndef RT_MESH_WAVES
 #define RT_MESH_WAVES 4
+#endif
+// shading kernels (GENERAL, the reference's default mode): a floor of 4 waves
+// per SIMD. The mesh's takes 135 VGPRs (3 waves) on its own; at 4 it gets 127
+// and spills 12 B per lane, and is faster: bunny default mode 1080p, 8 frames
+// x 2 / x 1 streams, 0.2267 -> 0.2068 / 0.2877 -> 0.2738 ms/frame (same box).
+// 1 = the compiler's choice (A/B switch).
+#ifndef RT_GENERAL_WAVES
+#define RT_GENERAL_WAVES 4
 #endif
 struct MeshS {
   static constexpr int kFields = 3;
@@ -426,7 +434,7 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
 // Trees deeper than 7 slots are LDS-limited anyway.
 template <class S, int SLOTS, bool GENERAL, int DIAG>
 constexpr int min_waves() {
-  return (GENERAL || DIAG != 0 || SLOTS > 7) ? 1 : S::kMinWaves;
+  return (DIAG != 0 || SLOTS > 7) ? 1 : GENERAL ? RT_GENERAL_WAVES : S::kMinWaves;
 }
 
 template <class S, int SLOTS, bool GENERAL, int DIAG>

@@ -86,16 +86,20 @@ __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uin
 
 // One leaf: its local best, first wins among equal t (strict `>` in triangle
 // order, triangles_raytracing.cpp:324-331). The leaf's triangles are read in
-// batches of RT_LEAF_BATCH with all their loads in flight together (the
-// triangle array is padded by 8 entries, so reading past a short leaf is in
-// bounds and the extra lanes are discarded), instead of one memory round trip
-// per triangle. Triangles per batch: 2 frees the VGPRs
-// the 4-wave mesh kernel needs (RT_MESH_WAVES, rt_device.hip); at the
-// compiler's 3 waves, 4 per batch is faster (bunny 0.1191 vs 0.1234 ms).
+// batches of B with all their loads in flight together (the triangle array is
+// padded by 8 entries, so reading past a short leaf is in bounds and the extra
+// lanes are discarded), instead of one memory round trip per triangle. The
+// primary-ray kernels take batches of RT_LEAF_BATCH_PRIMARY = 4 (127 VGPRs, 4
+// waves; bunny 0.1088 -> 0.1074, 1.1 M tris 4K 0.4292 -> 0.4244 ms/frame
+// against 2); the shading kernels keep RT_LEAF_BATCH = 2, where 4 takes them
+// from 3 waves (136 VGPRs) to 2 (181).
 #ifndef RT_LEAF_BATCH
 #define RT_LEAF_BATCH 2
 #endif
-template <class CT>
+#ifndef RT_LEAF_BATCH_PRIMARY
+#define RT_LEAF_BATCH_PRIMARY 4
+#endif
+template <uint32_t B = RT_LEAF_BATCH, class CT>
 __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, uint32_t w, f3 o,
                                           f3 d, float &lt, uint32_t &lk, CT &cnt) {
   const uint32_t first = (w >> 3) & rtl::kMaxLeafFirstTri;
@@ -103,7 +107,6 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
   cnt.add(C_BVH_LEAF, 1);
   cnt.add(C_BVH_TRI, n);
   const float4 *q = reinterpret_cast<const float4 *>(tris + first);
-  constexpr uint32_t B = RT_LEAF_BATCH;
   for (uint32_t base = 0; base < n; base += B) {
     float4 a[B], b[B], c[B];
 #pragma unroll
@@ -130,6 +133,15 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
 #ifndef RT_EXPAND_FAST
 #define RT_EXPAND_FAST 1
 #endif
+// 1: the fast list also covers waves whose rays each enter at most 3 children
+// with distinct t (A/B switch)
+#ifndef RT_SORT3
+#define RT_SORT3 0
+#endif
+// 1: child slots empty in every lane of the wave skip their slab test (A/B switch)
+#ifndef RT_SLOT_SKIP
+#define RT_SLOT_SKIP 0
+#endif
 template <bool FAST>
 __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node, f3 o, f3 inv,
                                             float tNear, float tFar, uint32_t &list,
@@ -148,13 +160,66 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
+#if RT_SLOT_SKIP
+    // an empty slot (child word kInvalidChild, box all +inf: t = -1 for every
+    // ray) in every lane of the wave skips its slab test
+    if (c > 0 && __ballot(cws[c] != rtl::kInvalidChild) == 0) {
+      t[c] = -1.0f;
+      id[c] = (uint32_t)c;
+      continue;
+    }
+#endif
     t[c] = slab<FAST>(bx[6 * c], bx[6 * c + 2], bx[6 * c + 4], bx[6 * c + 1], bx[6 * c + 3],
                       bx[6 * c + 5], o, inv, tNear, tFar);  // box: xMin xMax yMin yMax zMin zMax
     id[c] = (uint32_t)c;
   }
   uint32_t first_id = 0;
   bool sorted = false;
-  if constexpr (FAST && RT_EXPAND_FAST) {
+#if RT_SORT3
+  if constexpr (FAST) {
+    // every lane enters at most 3 children with distinct t: any correct sort
+    // lists them ascending, so a 3-comparator sort of the entered ones gives
+    // the network's list
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) m |= (t[c] < 0.0f) ? 0u : (1u << c);
+    const uint32_t pc = (uint32_t)__builtin_popcount(m);
+    const uint32_t ia = (uint32_t)__builtin_ctz(m | 0x100u), ic = 31u - (uint32_t)__builtin_clz(m | 1u);
+    const uint32_t mb = m & ~(1u << ia) & ~(1u << ic);
+    const uint32_t ib = (uint32_t)__builtin_ctz(mb | 0x100u);
+    float ta = t[0], tb = t[0], tc = t[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) {
+      ta = (ia == (uint32_t)c) ? t[c] : ta;
+      tb = (ib == (uint32_t)c) ? t[c] : tb;
+      tc = (ic == (uint32_t)c) ? t[c] : tc;
+    }
+    // entries: pc = 1: a; pc = 2: a, c; pc = 3: a, b, c
+    const bool slow = pc > 3 || (pc >= 2 && !(ta != tc)) || (pc == 3 && (!(ta != tb) || !(tb != tc)));
+    if (__ballot(slow) == 0) {
+      sorted = true;
+      float k0 = ta, k1 = pc == 3 ? tb : tc, k2 = tc;
+      uint32_t d0 = ia, d1 = pc == 3 ? ib : ic, d2 = ic;
+      auto cs = [](float &x, uint32_t &dx, float &y, uint32_t &dy) {
+        const bool sw = x > y;
+        const float tt = x; x = sw ? y : x; y = sw ? tt : y;
+        const uint32_t u = dx; dx = sw ? dy : dx; dy = sw ? u : dy;
+      };
+      if (pc == 3) {
+        cs(k0, d0, k1, d1);
+        cs(k1, d1, k2, d2);
+        cs(k0, d0, k1, d1);
+      } else {
+        cs(k0, d0, k1, d1);  // pc = 2 (k1 = tc); pc <= 1 leaves k0 first
+      }
+      first_id = d0;
+      tfirst = pc == 0 ? 0.0f : k0;
+      cnt = pc;
+      list = pc == 0 ? 0u : pc == 1 ? d0 : pc == 2 ? (d0 | (d1 << 3)) : (d0 | (d1 << 3) | (d2 << 6));
+    }
+  }
+#endif
+  if constexpr (FAST && RT_EXPAND_FAST && !RT_SORT3) {
     // At most two children entered with distinct t: the network's output order
     // of the entered children is plain ascending t (any correct sort gives
     // it), so the wave skips sort8 when every lane is in that case. Ties (or
@@ -263,7 +328,7 @@ constexpr int kCoopRays = 8;
 // "while-while" split into an inner-node phase and a leaf phase: bunny
 // 0.342 -> 0.523 ms.) TAIL: before each iteration, if kCoopRays or fewer lanes
 // of the wave are still looping, store the state and return true (suspended).
-template <int BLOCK, bool ANY, bool FAST, bool TAIL, class CT>
+template <int BLOCK, bool ANY, bool FAST, bool TAIL, uint32_t LB = RT_LEAF_BATCH, class CT>
 __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                          LdsStack<BLOCK> st, MState &S, CT &cnt) {
   uint32_t word = S.word, flist = S.flist, fcnt = S.fcnt, fnode = S.fnode, cwnext = S.cwnext, gk = S.gk;
@@ -277,7 +342,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       if (word & rtl::kLeafBit) {
         float lt = kInf;
         uint32_t lk = rtl::kInvalidChild;
-        leaf_test(sc.tris, word, o, d, lt, lk, cnt);
+        leaf_test<LB>(sc.tris, word, o, d, lt, lk, cnt);
         if (lk != rtl::kInvalidChild) {
           if (ANY) { gbest = lt; gk = lk; break; }
           if (lt < fbest) fbest = lt;
@@ -553,11 +618,11 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   }
   bool suspended = false;
   if (pending && sc.coop)
-    suspended = fast ? mesh_run<BLOCK, false, true, true>(sc, o, d, inv, tNear, tFar, st, S, cnt)
-                     : mesh_run<BLOCK, false, false, true>(sc, o, d, inv, tNear, tFar, st, S, cnt);
+    suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
+                     : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt);
   else if (pending)
-    (void)(fast ? mesh_run<BLOCK, false, true, false>(sc, o, d, inv, tNear, tFar, st, S, cnt)
-                : mesh_run<BLOCK, false, false, false>(sc, o, d, inv, tNear, tFar, st, S, cnt));
+    (void)(fast ? mesh_run<BLOCK, false, true, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
+                : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt));
   // Rays still traversing: at most kCoopRays per branch of the fast/exact
   // dispatch above (each branch suspends on its own lane count), so up to
   // 2 * kCoopRays; they are finished kCoopRays at a time.
