@@ -1181,6 +1181,18 @@ bool persist_enabled() {
   return on;
 }
 
+// row-band launches of up to this many ranks take the work queue too
+// (RTAMD_BAND_PERSIST=<N>, A/B switch). Bunny 1080p, max over ranks, 8 frames
+// x 2 streams (ms/frame, queue vs blocks): N = 2 0.0595 vs 0.0607, N = 4
+// 0.0425 vs 0.0342, N = 8 0.0379 vs 0.0218.
+int band_persist_max() {
+  static const int v = [] {
+    const char *e = std::getenv("RTAMD_BAND_PERSIST");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 // wave tiles per queue item (0: block dispatch); RTAMD_PERSIST_G=1|2|4 overrides
 // the scene's default (A/B switch)
 int persist_group(int dflt) {
@@ -1290,13 +1302,12 @@ int launch_pump_t(const P &sc, const FrameBatch &fb, int n, int group, hipStream
 template <class S, int MAXD>
 int launch_batch_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
                    hipStream_t stream) {
-  // Row-band tiles (a rank's share of a multi-GPU frame) take the block
-  // dispatch: with 1/N of the pixels per launch the queue's drain (a wave
-  // probes all 8 heads before it exits) and its launch-to-launch hand-over
-  // cost more than they balance (bunny 1080p, rank 0 of 4: 0.0415 vs 0.0336
-  // ms/frame; of 8: 0.037 vs 0.021; at N = 2 the two are level).
+  // Row-band tiles (a rank's share of a multi-GPU frame) of more than 2 ranks
+  // take the block dispatch: with 1/N of the pixels per launch the queue's
+  // drain (a wave probes all 8 heads before it exits) and its launch-to-launch
+  // hand-over cost more than they balance (band_persist_max).
   const int group = persist_group(S::kQueueGroup);
-  if (persist_enabled() && group > 0 && fb.f[0].nranks <= 1) {
+  if (persist_enabled() && group > 0 && fb.f[0].nranks <= band_persist_max()) {
     if constexpr (PumpOf<S>::kHas) {
       if (!general && (pump_env() || (s && s->pump_on)))
         return launch_pump_t<typename PumpOf<S>::P, MAXD>(PumpOf<S>::make(sc), fb, n, group, stream);
