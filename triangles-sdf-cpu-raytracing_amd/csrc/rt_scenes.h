@@ -1169,7 +1169,10 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
 // Traversal state of one octree ray below the root expansion: the top frame
 // (the children block (childrenOffset) of the node whose children are being
 // visited, its remaining list, the leaf mask of that block and its
-// coordinates) lives here, the frames below it in LDS slots [0, depth-1].
+// coordinates) lives here, the frames below it in LDS slots [0, sp-1]. A frame
+// whose list is used up is not pushed (the descent into a block's last child
+// is a tail call), so a frame records its depth, and a pop always finds a
+// child to visit: it falls through to that visit in the same iteration.
 // Frames keep the block, not the node, so visiting a child costs one dependent
 // load (its word, or a leaf's corner values), not two. The state is
 // resumable: oct_run can suspend a ray between two iterations and continue it
@@ -1190,6 +1193,7 @@ struct OctRay {
   uint32_t leafm;  // children of the top frame that are leaves that can hit (masked walk)
   uint32_t ix, iy, iz;
   int32_t depth;  // depth of the top frame's node (root = 0)
+  int32_t sp;     // frames on the LDS stack
 };
 // ray status: still traversing (suspended), finished without a hit, with a hit
 enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
@@ -1215,7 +1219,7 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
   uint32_t l, c;
   oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, CT::kCounts ? 0xFFu : (rw.masks & 0xFFu), l, c);
-  R = OctRay{root, l | (c << 24), rw.masks >> 8, 0u, 0u, 0u, 0};
+  R = OctRay{root, l | (c << 24), rw.masks >> 8, 0u, 0u, 0u, 0, 0};
   return c == 0 ? RAY_MISS : RAY_PENDING;
 }
 
@@ -1229,22 +1233,25 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
   constexpr bool MASKS = !CT::kCounts;
   uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24, leafm = R.leafm;
   uint32_t ix = R.ix, iy = R.iy, iz = R.iz;
-  int depth = R.depth;
+  int depth = R.depth, sp = R.sp;
   for (;;) {
     if (SUSPEND && __popcll(__ballot(1)) <= limit) {
-      R = OctRay{fbase, flist | (fcnt << 24), leafm, ix, iy, iz, depth};
+      R = OctRay{fbase, flist | (fcnt << 24), leafm, ix, iy, iz, depth, sp};
       return RAY_PENDING;
     }
     if (fcnt == 0) {
-      if (depth == 0) return RAY_MISS;
-      --depth;
-      fbase = st.at(depth, 0);
-      const uint32_t lc = st.at(depth, 1);
-      if (MASKS) leafm = st.at(depth, 2);
+      if (sp == 0) return RAY_MISS;
+      --sp;
+      fbase = st.at(sp, 0);
+      const uint32_t lc = st.at(sp, 1);
+      const uint32_t w2 = st.at(sp, 2);  // leaf mask | depth << 8
+      if (MASKS) leafm = w2 & 0xFFu;
+      const int d2 = (int)(w2 >> 8);
+      const uint32_t sh = (uint32_t)(depth - d2);
+      ix >>= sh; iy >>= sh; iz >>= sh;
+      depth = d2;
       flist = lc & 0xFFFFFFu;
-      fcnt = lc >> 24;
-      ix >>= 1; iy >>= 1; iz >>= 1;
-      continue;
+      fcnt = lc >> 24;  // >= 1: empty frames are never pushed
     }
     const uint32_t j = flist & 7u;
     flist >>= 3;
@@ -1277,9 +1284,12 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     uint32_t l, c;
     oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, MASKS ? (cw.masks & 0xFFu) : 0xFFu, l, c);
     if (c == 0) continue;
-    st.at(depth, 0) = fbase;
-    st.at(depth, 1) = flist | (fcnt << 24);
-    if (MASKS) st.at(depth, 2) = leafm;
+    if (fcnt != 0) {
+      st.at(sp, 0) = fbase;
+      st.at(sp, 1) = flist | (fcnt << 24);
+      st.at(sp, 2) = (MASKS ? leafm : 0u) | ((uint32_t)depth << 8);
+      ++sp;
+    }
     ++depth;
     fbase = cw.child; flist = l; fcnt = c;
     leafm = cw.masks >> 8;
