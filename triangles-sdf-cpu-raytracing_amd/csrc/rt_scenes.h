@@ -354,12 +354,23 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
         cnt.add(C_BVH_INNER, 1);
         expand_node<FAST>(sc.nodes + word, o, inv, tNear, tFar, l, c, tf, cwf);
         if (c != 0) {
-          if (depth >= 1) {
-            st.at(depth - 1, 0) = fnode;
-            st.at(depth - 1, 1) = flist | (fcnt << 24);
-            st.at(depth - 1, 2) = __float_as_uint(fbest);
+          if (depth >= 1 && fcnt == 0) {
+            // tail call: the top frame has no child left, so it is replaced,
+            // not pushed; its best folds into the frame below now (that frame
+            // reads it only when it resumes, after this whole subtree, and
+            // min is associative: the same best as folding on return)
+            if (depth >= 2) {
+              const float below = __uint_as_float(st.at(depth - 2, 2));
+              if (fbest < below) st.at(depth - 2, 2) = __float_as_uint(fbest);
+            }
+          } else {
+            if (depth >= 1) {
+              st.at(depth - 1, 0) = fnode;
+              st.at(depth - 1, 1) = flist | (fcnt << 24);
+              st.at(depth - 1, 2) = __float_as_uint(fbest);
+            }
+            ++depth;
           }
-          ++depth;
           fnode = word; flist = l; fcnt = c; fbest = kInf;
           tnext = tf;
           cwnext = cwf;
@@ -380,7 +391,9 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       fbest = __uint_as_float(st.at(depth - 1, 2));
       if (child_best < fbest) fbest = child_best;
       have_t = false;
-      continue;
+      // frames reach the stack with a child left (mesh_run_coop may still
+      // push one without: then the next iteration pops again)
+      if (fcnt == 0) continue;
     }
     const uint32_t j = flist & 7u;
     flist >>= 3;
