@@ -391,9 +391,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       fbest = __uint_as_float(st.at(depth - 1, 2));
       if (child_best < fbest) fbest = child_best;
       have_t = false;
-      // frames reach the stack with a child left (mesh_run_coop may still
-      // push one without: then the next iteration pops again)
-      if (fcnt == 0) continue;
+      // stacked frames always have a child left: go on to it
     }
     const uint32_t j = flist & 7u;
     flist >>= 3;
@@ -553,12 +551,19 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
         const uint32_t idf = __shfl(id, gbase + (int)(i0 & 7u), 64);
         const uint32_t cwf = __shfl(cwk, gbase + (int)idf, 64);
         if (c != 0) {
-          if (depth >= 1) {
-            st.at(depth - 1, 0) = fnode;
-            st.at(depth - 1, 1) = flist | (fcnt << 24);
-            st.at(depth - 1, 2) = __float_as_uint(fbest);
+          if (depth >= 1 && fcnt == 0) {  // tail call, as in mesh_run
+            if (depth >= 2) {
+              const float below = __uint_as_float(st.at(depth - 2, 2));
+              if (fbest < below) st.at(depth - 2, 2) = __float_as_uint(fbest);
+            }
+          } else {
+            if (depth >= 1) {
+              st.at(depth - 1, 0) = fnode;
+              st.at(depth - 1, 1) = flist | (fcnt << 24);
+              st.at(depth - 1, 2) = __float_as_uint(fbest);
+            }
+            ++depth;
           }
-          ++depth;
           fnode = word; flist = l; fcnt = c; fbest = kInf;
           tnext = tf;
           cwnext = cwf;
@@ -579,7 +584,6 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
       fbest = __uint_as_float(st.at(depth - 1, 2));
       if (child_best < fbest) fbest = child_best;
       have_t = false;
-      continue;
     }
     const uint32_t j = flist & 7u;
     flist >>= 3;
