@@ -319,6 +319,12 @@ struct MState {
   bool have_t;
 };
 
+// Frame ends by pruning handled per traversal iteration (1: one; the next
+// iteration pops the ended frame; A/B switch)
+#ifndef RT_MESH_PRUNE_PASSES
+#define RT_MESH_PRUNE_PASSES 1
+#endif
+
 // Rays still looping in a wave at or below which the primary mesh path hands
 // its remaining rays to 8-lane groups (mesh_run_coop).
 constexpr int kCoopRays = 8;
@@ -379,32 +385,39 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       }
       word = rtl::kInvalidChild;
     }
-    if (depth == 0) break;
-    if (fcnt == 0) {  // frame done: fold its best into the parent frame
-      --depth;
-      if (depth == 0) break;
-      const float child_best = fbest;
-      fnode = st.at(depth - 1, 0);
-      const uint32_t lc = st.at(depth - 1, 1);
-      flist = lc & 0xFFFFFFu;
-      fcnt = lc >> 24;
-      fbest = __uint_as_float(st.at(depth - 1, 2));
-      if (child_best < fbest) fbest = child_best;
+    // choose the next child; a pruned child ends its frame, and up to
+    // RT_MESH_PRUNE_PASSES - 1 such ends are popped in this same iteration
+    bool done = false;
+#pragma unroll
+    for (int pass = 0; pass < RT_MESH_PRUNE_PASSES; ++pass) {
+      if (depth == 0) { done = true; break; }
+      if (fcnt == 0) {  // frame done: fold its best into the parent frame
+        --depth;
+        if (depth == 0) { done = true; break; }
+        const float child_best = fbest;
+        fnode = st.at(depth - 1, 0);
+        const uint32_t lc = st.at(depth - 1, 1);
+        flist = lc & 0xFFFFFFu;
+        fcnt = lc >> 24;
+        fbest = __uint_as_float(st.at(depth - 1, 2));
+        if (child_best < fbest) fbest = child_best;
+        have_t = false;
+        // stacked frames always have a child left: go on to it
+      }
+      const uint32_t j = flist & 7u;
+      flist >>= 3;
+      fcnt -= 1;
+      if (!have_t) {  // resumed frame: child box and word, loaded together
+        const rtl::GNode *nd = sc.nodes + fnode;
+        const float *b = nd->box[j];
+        cwnext = nd->child[j];
+        tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
+      }
       have_t = false;
-      // stacked frames always have a child left: go on to it
+      if (!(fbest < tnext)) { word = cwnext; break; }
+      fcnt = 0;  // pruned; later siblings have larger t
     }
-    const uint32_t j = flist & 7u;
-    flist >>= 3;
-    fcnt -= 1;
-    if (!have_t) {  // resumed frame: child box and word, loaded together
-      const rtl::GNode *nd = sc.nodes + fnode;
-      const float *b = nd->box[j];
-      cwnext = nd->child[j];
-      tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
-    }
-    have_t = false;
-    if (fbest < tnext) { fcnt = 0; continue; }  // pruned; later siblings have larger t
-    word = cwnext;
+    if (done) break;
   }
   S.word = word; S.flist = flist; S.fcnt = fcnt; S.fnode = fnode; S.cwnext = cwnext; S.gk = gk;
   S.fbest = fbest; S.tnext = tnext; S.gbest = gbest; S.depth = depth; S.have_t = have_t;
