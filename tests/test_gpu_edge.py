@@ -103,3 +103,40 @@ def test_random_cameras(gpu, name):
         up = (0.0, 1.0, 0.0) if k % 3 else tuple(rng.normal(size=3).astype(np.float32).tolist())
         mode = ("primary", "default", "color")[k % 3]
         same(*frames(ref_s, gpu_s, 96, 64, pos, mode, off, up=up), f"{name} cam {k} {pos} {mode}")
+
+
+@pytest.mark.parametrize("force", [0, 1, 2, 3])
+def test_grid_address_paths(gpu, force):
+    """Every grid_mode branch (linear / bricked layout x 32-bit buffer / 64-bit
+    address loads), forced on the shipped 65^3 grid with rtx_set_grid_force:
+    frames and IScene::intersect bitwise equal to the oracle's."""
+    import ctypes as C
+
+    import scenes as S
+    from rtamd import _lib
+    L = rtamd.lib()
+    L.rtx_set_grid_force.argtypes = [C.c_int]
+    name = "example_grid.grid"
+    size, vals = S.inputs(name)[1]
+    ref_s = S.ref_scene(name)
+    _lib.check(L.rtx_set_grid_force(force))
+    try:
+        gpu_s = rtamd.SDFGrid(size, vals)  # created under the forced layout
+        for mode in ("primary", "default"):
+            same(*frames(ref_s, gpu_s, 160, 90, (0.4, 0.3, 2.4), mode), f"force {force} {mode}")
+        rng = np.random.default_rng(7 + force)
+        o = rng.uniform(-2.5, 2.5, (4000, 3)).astype(np.float32)
+        d = rng.normal(size=(4000, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+        ref_s.set_plane(False, (0, 1, 0), 0.0)
+        gpu_s.set_plane(None)
+        rh, rt_, rn, rp = ref_s.intersect_rays(o, d, 0.01, 100.0)
+        g = gpu_s.intersect(o, d, 0.01, 100.0)
+        assert np.array_equal(rh.astype(bool), g.hitten)
+        assert np.array_equal(rp, g.prim)
+        h = g.hitten
+        assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32))
+        assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32))
+        gpu_s.close()
+    finally:
+        _lib.check(L.rtx_set_grid_force(0))

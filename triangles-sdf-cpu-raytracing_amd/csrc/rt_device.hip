@@ -955,10 +955,17 @@ uint64_t grid_samples(const rt_scene *s) {
   return s->grid_bricked ? grid_bricked_samples(s->size) : (uint64_t)s->size[0] * s->size[1] * s->size[2];
 }
 
+// diagnostic (rtx_set_grid_force): bit 0 = grids created from now on take the
+// bricked layout whatever their size, bit 1 = every grid launch takes the 64-bit
+// address path (no buffer loads); tests reach each grid_mode branch with it
+int g_grid_force = 0;
+
 GridDev grid_dev(const rt_scene *s) {
   const uint64_t n = grid_samples(s);
-  // buffer loads address up to 4 GiB (32-bit offsets, num_records saturated at 2^32-1)
-  const uint32_t bytes = 4 * n <= (1ull << 32) ? (uint32_t)std::min<uint64_t>(4 * n, 0xFFFFFFFFull) : 0u;
+  // buffer loads: 32-bit byte offsets and num_records, so only grids below
+  // 4 GiB (a grid of exactly 2^32 bytes would put its last sample past a
+  // saturated num_records) -- larger ones take the 64-bit address path
+  const uint32_t bytes = 4 * n < (1ull << 32) ? (uint32_t)(4 * n) : 0u;
   if (!s->grid_bricked) return GridDev{s->d_vals, s->size[0], s->size[1], s->size[2], s->size[2],
                                        s->size[1] * s->size[2], bytes};
   const uint32_t ys = grid_bricks(s->size[2]) * 64u;
@@ -967,7 +974,7 @@ GridDev grid_dev(const rt_scene *s) {
 
 int grid_mode(const rt_scene *s, const GridDev &gd) {
   // buffer mode: 32-bit byte offsets and 24-bit stride multiplies (grid_mul)
-  const bool buf = gd.bytes != 0 && gd.xs < (1u << 24) && gd.ys < (1u << 24);
+  const bool buf = gd.bytes != 0 && gd.xs < (1u << 24) && gd.ys < (1u << 24) && !(g_grid_force & 2);
   return (buf ? kGridBuf : 0) | (s->grid_bricked ? kGridBricked : 0);
 }
 
@@ -1589,7 +1596,7 @@ int rt_scene_create_grid(const uint32_t size[3], const float *values, rt_scene *
   if (rc) return rc;
   s->kind = RT_SCENE_GRID;
   s->size[0] = size[0]; s->size[1] = size[1]; s->size[2] = size[2];
-  if ((uint64_t)n * 4 <= kGridLinearMaxBytes) {  // fits one XCD's L2: the reference layout
+  if ((uint64_t)n * 4 <= kGridLinearMaxBytes && !(g_grid_force & 1)) {  // fits one XCD's L2: the reference layout
     if ((rc = upload(&s->d_vals, values, (size_t)n, s->dev_bytes))) {
       rt_scene_destroy(s);
       return rc;
@@ -2063,6 +2070,14 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
   g_persist_stamps = (unsigned long long *)d_buf;
   g_persist_stamps_cap = d_buf ? cap_waves : 0;
+  return RT_OK;
+}
+
+// Diagnostic: force grid layouts / address paths (g_grid_force bits). Not part
+// of include/rtamd.h.
+int rtx_set_grid_force(int flags) {
+  if (flags < 0 || flags > 3) return set_err(RT_E_INVALID, "grid force flags must be 0..3");
+  g_grid_force = flags;
   return RT_OK;
 }
 
