@@ -140,3 +140,30 @@ def test_grid_address_paths(gpu, force):
         gpu_s.close()
     finally:
         _lib.check(L.rtx_set_grid_force(0))
+
+
+@pytest.mark.parametrize("seed,ntri,mode", [(11, 2000, "grid"), (12, 3000, "rand"), (13, 1500, "same"),
+                                            (14, 2500, "flat")])
+def test_overlapping_meshes_random_rays(gpu, seed, ntri, mode):
+    """IScene::intersect on meshes whose BVH8 boxes overlap heavily and whose
+    triangles tie (axis-aligned lattice, duplicates, one plane): the traversal's
+    per-frame local best, its fold on return (or at a tail-call descent) and
+    the first-found tie rule must give the oracle's hit, t, normal and id."""
+    v, i = tri_mesh(seed, ntri, mode)
+    ref_s, gpu_s = cpuref.RefScene.mesh(v, i), rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    rng = np.random.default_rng(seed)
+    n = 30000
+    o = rng.uniform(-2.0, 2.0, (n, 3)).astype(np.float32)
+    inside = rng.random(n) < 0.4
+    o[inside] = rng.uniform(-0.6, 0.6, (int(inside.sum()), 3)).astype(np.float32)
+    d = (rng.uniform(-0.7, 0.7, (n, 3)) - o).astype(np.float32)  # mostly towards the model
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    for tn, tf in ((0.01, 100.0), (-3.0, 100.0)):
+        rh, rt_, rn, rp = ref_s.intersect_rays(o, d, tn, tf)
+        g = gpu_s.intersect(o, d, tn, tf)
+        assert rh.sum() > n // 10
+        assert np.array_equal(rh.astype(bool), g.hitten), f"{mode} tn={tn}: hit mask"
+        assert np.array_equal(rp, g.prim), f"{mode} tn={tn}: primitive ids"
+        h = g.hitten
+        assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), f"{mode} tn={tn}: t"
+        assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), f"{mode} tn={tn}: normal"
