@@ -327,7 +327,10 @@ struct MState {
 
 // Rays still looping in a wave at or below which the primary mesh path hands
 // its remaining rays to 8-lane groups (mesh_run_coop).
-constexpr int kCoopRays = 8;
+#ifndef RT_COOP_RAYS
+#define RT_COOP_RAYS 8  // A/B switch (0: never hand over)
+#endif
+constexpr int kCoopRays = RT_COOP_RAYS;
 
 // The traversal loop. One iteration = one unit of this lane's work (expand a
 // node, test a leaf, or resume/pop a frame). (Measured and rejected: the
