@@ -83,7 +83,6 @@ struct MeshS {
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   static constexpr int kMinWaves = RT_MESH_WAVES;
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
-  static constexpr int kQueueBand = 0;   // queue order: item rows per band, 0 = frame after frame
   MeshDev d;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
@@ -118,7 +117,6 @@ struct GridS {
   // block dispatch: a grid tile is too short for the queue's claims to pay
   // (256^3, 8 frames x 2 streams: 0.0506 ms/frame vs 0.0541 at 4 tiles per claim)
   static constexpr int kQueueGroup = 0;
-  static constexpr int kQueueBand = 0;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -136,7 +134,6 @@ struct OctS {
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   static constexpr int kQueueGroup = 2;
-  static constexpr int kQueueBand = 0;
   OctDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -487,9 +484,6 @@ struct PersistQ {
   uint32_t waves;    // waves in the grid
   uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
   uint32_t stride;   // words between heads
-  // queue order: 0 = frame after frame; else bands of `band` items taken from
-  // every frame in turn (band 0 of frames 0..n-1, band 1 of frames 0..n-1, ...)
-  uint32_t band, frames;
   // diagnostic builds (-DRT_PERSIST_STAMPS, tools/build_variant.sh; see
   // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 8 x u64 =
   // start, end (s_memrealtime, 100 MHz), items traced | XCD << 32, end of its
@@ -501,30 +495,6 @@ struct PersistQ {
 // (RTAMD_QSTRIDE=<words> overrides it for A/B runs, at most kHeadStrideMax)
 constexpr int kHeadStride = 1088;
 constexpr int kHeadStrideMax = 4096;
-
-// item -> (frame, item within the frame) under the queue order (wave-uniform,
-// scalar arithmetic). Band order starts every frame's heavy middle rows (the
-// silhouette items, DESIGN.md section 4 tail) near the middle of the launch
-// instead of leaving the last frame's for its end; the per-frame remainder of
-// partial bands comes last, frame after frame.
-__device__ __forceinline__ void q_decode(const PersistQ &q, uint32_t item, uint32_t &f, uint32_t &r) {
-  if (q.band == 0) {
-    f = item / q.per_frame;
-    r = item - f * q.per_frame;
-    return;
-  }
-  const uint32_t full = q.per_frame / q.band * q.band;  // items of a frame in whole bands
-  const uint32_t head = full * q.frames;
-  if (item < head) {
-    const uint32_t span = q.band * q.frames, s = item / span, o = item - s * span;
-    f = o / q.band;
-    r = s * q.band + (o - f * q.band);
-  } else {
-    const uint32_t rem = q.per_frame - full, o = item - head;
-    f = o / rem;
-    r = full + (o - f * rem);
-  }
-}
 
 __device__ __forceinline__ uint32_t q_claim(uint32_t *head) {
   uint32_t k = 0;
@@ -563,8 +533,7 @@ void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
       continue;
     }
     const uint32_t knext = q_claim(q.heads + h * q.stride);
-    uint32_t f, r;
-    q_decode(q, item, f, r);
+    const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
 #ifdef RT_PERSIST_STAMPS
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1241,19 +1210,6 @@ int persist_group(int dflt) {
   return (g == 1 || g == 2 || g == 4) ? g : dflt;
 }
 
-// Queue order of the persistent launches: item rows per band (0 = frame after
-// frame); rtx_set_queue_band(rows) or RTAMD_QBAND=<rows> overrides the scene's
-// default (diagnostic / A/B switch).
-int g_queue_band = -1;
-template <class S>
-int queue_band_rows(const S &) {
-  static const int v = [] {
-    const char *e = std::getenv("RTAMD_QBAND");
-    return e ? std::atoi(e) : -1;
-  }();
-  return g_queue_band >= 0 ? g_queue_band : v >= 0 ? v : S::kQueueBand;
-}
-
 // Resident workgroups of a persistent kernel on the current device (cached per
 // kernel instantiation and device).
 template <class K>
@@ -1274,7 +1230,7 @@ int resident_blocks(K kernel, int &blocks, int &dev_cached) {
 // (1: 1x1, 2: 2x1, 4: 2x2) of n frames, the stream's head set; *grid = the
 // launch's workgroups (the resident ones, fewer for a small batch).
 int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t stream, PersistQ &q,
-               uint32_t &grid, int band_rows = 0) {
+               uint32_t &grid) {
   uint32_t *heads = nullptr;
   if (const int rc = stream_queue(stream, &heads)) return rc;
   q.heads = heads;
@@ -1289,12 +1245,6 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   q.tiles_x = (uint32_t)((fb.f[0].W + 8 * q.gx - 1) / (8 * q.gx));
   q.per_frame = q.tiles_x * (uint32_t)((fb.f[0].rows_local + 8 * q.gy - 1) / (8 * q.gy));
   q.items = q.per_frame * (uint32_t)n;
-  q.frames = (uint32_t)n;
-  q.band = 0;
-  if (band_rows > 0 && n > 1) {
-    const uint32_t b = (uint32_t)band_rows * q.tiles_x;
-    q.band = b < q.per_frame ? b : 0;
-  }
   grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
   q.waves = grid * (kBlock / 64);
   q.stamps = (g_persist_stamps && (int64_t)q.waves <= g_persist_stamps_cap) ? g_persist_stamps : nullptr;
@@ -1308,7 +1258,7 @@ int launch_persist_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBa
   if (const int rc = resident_blocks(render_persist_kernel<S, MAXD, GENERAL>, blocks, dev_cached)) return rc;
   PersistQ q;
   uint32_t grid = 0;
-  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid, queue_band_rows(sc))) return rc;
+  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid)) return rc;
   render_persist_kernel<S, MAXD, GENERAL><<<grid, kBlock, 0, stream>>>(sc, pl, fb, q);
   return RT_OK;
 }
@@ -2128,15 +2078,6 @@ int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
 int rtx_set_grid_force(int flags) {
   if (flags < 0 || flags > 3) return set_err(RT_E_INVALID, "grid force flags must be 0..3");
   g_grid_force = flags;
-  return RT_OK;
-}
-
-// Diagnostic: queue order of the persistent launches from now on, in item rows
-// per band (0 = frame after frame, -1 = the scene's default). Not part of
-// include/rtamd.h.
-int rtx_set_queue_band(int rows) {
-  if (rows < -1) return set_err(RT_E_INVALID, "queue band rows must be >= -1");
-  g_queue_band = rows;
   return RT_OK;
 }
 
