@@ -83,6 +83,7 @@ struct MeshS {
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   static constexpr int kMinWaves = RT_MESH_WAVES;
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
+  static constexpr int kLdsNodes = RT_LDS_NODES;  // top-of-tree nodes per persistent block in LDS
   MeshDev d;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
@@ -117,6 +118,7 @@ struct GridS {
   // block dispatch: a grid tile is too short for the queue's claims to pay
   // (256^3, 8 frames x 2 streams: 0.0506 ms/frame vs 0.0541 at 4 tiles per claim)
   static constexpr int kQueueGroup = 0;
+  static constexpr int kLdsNodes = 0;
   GridDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -134,6 +136,7 @@ struct OctS {
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   static constexpr int kQueueGroup = 2;
+  static constexpr int kLdsNodes = 0;
   OctDev d;
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
@@ -504,8 +507,21 @@ __device__ __forceinline__ uint32_t q_claim(uint32_t *head) {
 
 template <class S, int SLOTS, bool GENERAL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
-void render_persist_kernel(S sc, PlaneDev pl, FrameBatch fb, PersistQ q) {
+void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  S sc = sc_arg;
+  if constexpr (S::kLdsNodes > 0 && !GENERAL) {
+    // the top BVH levels (the first inner nodes, BFS order) copied into this
+    // block's LDS once per launch; every item's traversal reads them there
+    constexpr int kQ = (int)(sizeof(rtl::GNode) / 16);
+    __shared__ float4 lnodes[S::kLdsNodes * kQ];
+    const uint32_t n = sc.d.n_inner < (uint32_t)S::kLdsNodes ? sc.d.n_inner : (uint32_t)S::kLdsNodes;
+    const float4 *src = reinterpret_cast<const float4 *>(sc.d.nodes);
+    for (uint32_t i = threadIdx.x; i < n * kQ; i += kBlock) lnodes[i] = src[i];
+    __syncthreads();
+    sc.d.lnodes = reinterpret_cast<const rtl::GNode *>(lnodes);
+    sc.d.n_lds = n;
+  }
   const int lane = threadIdx.x & 63;
   const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID: this wave's XCD
 #ifdef RT_PERSIST_STAMPS
@@ -912,6 +928,7 @@ struct rt_scene {
   uint32_t root = rtl::kInvalidChild;
   float root_box[6] = {0, 0, 0, 0, 0, 0};
   int64_t host_nodes = 0, host_inner = 0;
+  uint32_t n_inner = 0;  // inner nodes on the device (MeshDev::n_inner)
   int32_t bvh_depth = 0;
   // grid
   float *d_vals = nullptr;
@@ -993,7 +1010,7 @@ __global__ __launch_bounds__(256) void brick_kernel(const float *__restrict__ sr
 }
 
 MeshDev mesh_dev(const rt_scene *s) {
-  MeshDev m{s->d_nodes, s->d_tris, s->root, {}, s->coop};
+  MeshDev m{s->d_nodes, s->d_tris, s->root, {}, s->coop, s->n_inner, nullptr, 0};
   for (int k = 0; k < 6; ++k) m.rbox[k] = s->root_box[k];
   return m;
 }
@@ -1577,6 +1594,7 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
   s->host_nodes = b.host_nodes;
   s->host_inner = b.host_inner;
   s->bvh_depth = b.max_depth;
+  s->n_inner = (uint32_t)b.nodes.size();
   if ((rc = upload(&s->d_nodes, b.nodes.data(), b.nodes.size(), s->dev_bytes)) ||
       (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes))) {
     rt_scene_destroy(s);

@@ -59,7 +59,28 @@ struct MeshDev {
   // be fetched. Used only when all three 1/d components are finite.
   float rbox[6];
   bool coop;  // primary rays: cooperative tail enabled (diagnostic switch rtx_set_coop)
+  uint32_t n_inner;  // inner nodes (BFS order: the first ones are the top levels)
+  // top-of-tree copy in LDS (render_persist_kernel, RT_LDS_NODES): inner nodes
+  // [0, n_lds) are read from lnodes (a block's LDS), the rest from nodes
+  const rtl::GNode *lnodes;
+  uint32_t n_lds;
 };
+
+// Inner nodes of the top BVH levels kept in each persistent block's LDS (0:
+// off; A/B switch, e.g. 73 = the top three levels, 16 KiB per block). Node
+// reads then go through a per-lane choice of the LDS or the global copy (flat
+// loads). Bit-exact, and measured level to 1 % slower:
+// the vector L1 already serves 96-99 % of the node lines, so off.
+#ifndef RT_LDS_NODES
+#define RT_LDS_NODES 0
+#endif
+__device__ __forceinline__ const rtl::GNode *mesh_node(const MeshDev &sc, uint32_t i) {
+#if RT_LDS_NODES
+  return i < sc.n_lds ? sc.lnodes + i : sc.nodes + i;
+#else
+  return sc.nodes + i;
+#endif
+}
 
 // triangle_intersection (ray_pack.ispc:132-165) on one triangle already in
 // registers (v0, e1 = v1-v0, e2 = v2-v0; the subtractions are exact host-side
@@ -361,7 +382,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
         uint32_t l, c, cwf;
         float tf;
         cnt.add(C_BVH_INNER, 1);
-        expand_node<FAST>(sc.nodes + word, o, inv, tNear, tFar, l, c, tf, cwf);
+        expand_node<FAST>(mesh_node(sc, word), o, inv, tNear, tFar, l, c, tf, cwf);
         if (c != 0) {
           if (depth >= 1 && fcnt == 0) {
             // tail call: the top frame has no child left, so it is replaced,
@@ -411,7 +432,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       flist >>= 3;
       fcnt -= 1;
       if (!have_t) {  // resumed frame: child box and word, loaded together
-        const rtl::GNode *nd = sc.nodes + fnode;
+        const rtl::GNode *nd = mesh_node(sc, fnode);
         const float *b = nd->box[j];
         cwnext = nd->child[j];
         tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
@@ -552,7 +573,7 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
           if (tk < gbest) { gbest = tk; gk = first + kk; }
         }
       } else {
-        const rtl::GNode *nd = sc.nodes + word;
+        const rtl::GNode *nd = mesh_node(sc, word);
         const float2 *bp = reinterpret_cast<const float2 *>(nd->box[k]);
         const float2 bxx = bp[0], byy = bp[1], bzz = bp[2];  // (min, max) per axis
         const uint32_t cwk = nd->child[k];
@@ -605,7 +626,7 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
     flist >>= 3;
     fcnt -= 1;
     if (!have_t) {
-      const rtl::GNode *nd = sc.nodes + fnode;
+      const rtl::GNode *nd = mesh_node(sc, fnode);
       const float *b = nd->box[j];
       cwnext = nd->child[j];
       tnext = slab<FAST>(b[0], b[2], b[4], b[1], b[3], b[5], o, inv, tNear, tFar);
