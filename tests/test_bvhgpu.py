@@ -98,12 +98,23 @@ def test_device_builder_shipped_meshes(gpu, name):
 
 @pytest.mark.parametrize("seed,ntri,mode", [(1, 1, "rand"), (3, 9, "rand"), (4, 300, "rand"), (6, 64, "same"),
                                             (7, 500, "grid"), (8, 100, "flat"), (9, 30000, "grid"),
-                                            (10, 12000, "same"), (11, 40000, "rand"), (12, 150000, "grid")])
+                                            (10, 12000, "same"), (11, 40000, "rand"), (12, 150000, "grid"),
+                                            (13, 3000, "signed0"), (14, 40000, "signed0")])
 def test_device_builder_edge_meshes(gpu, seed, ntri, mode):
     """test_host.py's tie-heavy meshes: duplicate triangles (all keys tie),
-    integer lattices (many equal keys), flat meshes (zero-area boxes)."""
+    integer lattices (many equal keys), flat meshes (zero-area boxes), and
+    lattices whose zero coordinates are a random mix of -0.0 and +0.0: a child
+    box bound that is 0 must carry the sign bit calc_bbox gives it when the
+    node is created (triangles_raytracing.cpp:199), before the children's
+    sorts reorder the range."""
     rng = np.random.default_rng(seed)
-    if mode == "same":
+    if mode == "signed0":
+        g = rng.integers(-2, 3, size=(ntri, 3)).astype(np.float64)
+        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
+        z = (v == 0) & (rng.random(v.shape) < 0.5)
+        v[z] = -0.0
+        assert np.signbit(v[v == 0]).any() and (~np.signbit(v[v == 0])).any()
+    elif mode == "same":
         v = np.tile(rng.normal(size=(3, 3)), (ntri, 1))
     elif mode == "grid":
         g = rng.integers(0, 6, size=(ntri, 3)).astype(np.float64)
@@ -142,3 +153,41 @@ def test_device_built_scene_renders_golden_frame(gpu):
     t = np.full((H, W), np.inf, np.float32)
     sc.render(S.params("stanford-bunny.obj", W, H, "primary", module="gpu"), c, t, clear=True)
     assert cpuref.fnv1a64_words(c) == S.GOLDEN[("stanford-bunny.obj", 1920, 1080, "primary")]
+
+
+def test_auto_mode_falls_back_to_host_on_device_failure(gpu):
+    """AUTO mode (the default) builds meshes from 32,768 triangles on the device;
+    a device failure there (simulated by rtx_bvh_inject_failure) must not fail
+    scene creation: the host builder gives the identical tree. The forced
+    device mode reports the failure as RT_E_DEVICE with the HIP error text."""
+    import cpuref
+    import rtamd
+    L = rtamd.lib()
+    _, (v, i), _ = S.inputs("stanford-bunny.obj")
+    assert len(i) // 3 >= 32768
+    L.rtx_bvh_inject_failure(1)
+    try:
+        sc = rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    finally:
+        L.rtx_bvh_inject_failure(0)
+    assert L.rtx_bvh_last_builder() == 3  # host, after the device build failed
+    sc.set_plane(None)
+    W, H = 1920, 1080
+    c = np.zeros((H, W), np.uint32)
+    t = np.full((H, W), np.inf, np.float32)
+    sc.render(S.params("stanford-bunny.obj", W, H, "primary", module="gpu"), c, t, clear=True)
+    assert cpuref.fnv1a64_words(c) == S.GOLDEN[("stanford-bunny.obj", 1920, 1080, "primary")]
+    sc.close()
+    # without injection AUTO uses the device
+    sc2 = rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    assert L.rtx_bvh_last_builder() == 2
+    sc2.close()
+    # DEVICE mode: no fallback, a device error
+    rtamd._lib.check(L.rt_set_bvh_builder(2))
+    L.rtx_bvh_inject_failure(1)
+    try:
+        with pytest.raises(rtamd.RtError, match=r"error -3: GPU BVH build: injected failure: "):
+            rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    finally:
+        L.rtx_bvh_inject_failure(0)
+        rtamd._lib.check(L.rt_set_bvh_builder(0))

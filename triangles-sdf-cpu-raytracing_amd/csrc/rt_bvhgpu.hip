@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -594,7 +595,6 @@ struct PhaseTimer {
     acc[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
 };
-PhaseTimer g_pt;
 
 template <class T>
 struct DBuf {
@@ -614,6 +614,9 @@ struct DBuf {
   }
 };
 
+// rtx_bvh_inject_failure: the next N device builds fail as a device error would
+std::atomic<int> g_inject_fail{0};
+
 inline int lg2(uint64_t n) { return 63 - __builtin_clzll(n); }
 
 struct Sorter {
@@ -624,6 +627,8 @@ struct Sorter {
   DBuf<uint32_t> size, offs, sw, af, bf, Ai, Bi, segv, Lpos, Rpos, bsum, ctr;
   DBuf<float> kp;
   hipStream_t st = nullptr;
+  PhaseTimer own_pt;             // per build: concurrent builds share no state
+  PhaseTimer *pt = &own_pt;
 
   int init(uint32_t ntri, uint32_t *ids3, const float *keys3) {
     n = ntri;
@@ -666,9 +671,9 @@ struct Sorter {
     uint32_t hc[3] = {0, 0, nser};  // next count, next E, serial count
     HIP_TRY(hipMemcpyAsync(ctr.p + 2, &hc[2], 4, hipMemcpyHostToDevice, st));
     Seg *cur = segA.p, *nxt = segB.p;
-    g_pt.start();
+    pt->start();
     while (m > 0) {
-      ++g_pt.rounds;
+      ++pt->rounds;
       HIP_TRY(hipMemsetAsync(ctr.p, 0, 8, st));
       HIP_TRY(hipMemsetAsync(sw.p, 0, (size_t)m * 4, st));
       const uint32_t gm = (m + 255) / 256;
@@ -695,12 +700,12 @@ struct Sorter {
     }
     HIP_TRY(hipMemcpyAsync(&nser, ctr.p + 2, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    g_pt.stop(0);
-    g_pt.start();
+    pt->stop(0);
+    pt->start();
     if (nser) k_serial<<<nser, 64, 0, st>>>(serial.p, ids, K3, n);
-    ++g_pt.serial_launches;
+    ++pt->serial_launches;
     HIP_TRY(hipGetLastError());
-    g_pt.stop(1);
+    pt->stop(1);
     return RT_OK;
   }
 };
@@ -720,10 +725,22 @@ namespace rth {
 
 bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
                     std::string &err, bool with_canon) {
+  // every device-side failure is reported as "GPU BVH build: <step>: <HIP
+  // error>" (RT_E_DEVICE at the C ABI; in AUTO mode the host builder takes
+  // over); input errors carry no prefix (RT_E_INVALID)
   auto fail = [&](const char *what) {
     err = std::string("GPU BVH build: ") + what + ": " + rterr::get();
     return false;
   };
+  auto hfail = [&](const char *what, hipError_t e) {
+    err = std::string("GPU BVH build: ") + what + ": " + hipGetErrorString(e);
+    return false;
+  };
+#define BVH_DEV(expr, what)                     \
+  do {                                          \
+    const hipError_t e_ = (expr);               \
+    if (e_ != hipSuccess) return hfail(what, e_); \
+  } while (0)
   if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
   for (int64_t i = 0; i < nidx; ++i)
     if ((int64_t)idx[i] >= nverts) { err = "vertex index out of range"; return false; }
@@ -731,9 +748,13 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   if ((uint64_t)n > rtl::kMaxLeafFirstTri || 3ull * n >= (1ull << 31)) { err = "too many triangles"; return false; }
   out = BVHGpu();
   if (n == 0) { out.root_word = rtl::kInvalidChild; return true; }
+  if (g_inject_fail.load() > 0) {  // rtx_bvh_inject_failure: a simulated device failure
+    g_inject_fail.fetch_sub(1);
+    return hfail("injected failure", hipErrorOutOfMemory);
+  }
 
   const auto tb0 = std::chrono::steady_clock::now();
-  g_pt = PhaseTimer();
+  PhaseTimer pt;
   DBuf<float4> dv;
   DBuf<uint32_t> didx, ids3, backup, ddiv, dact;
   DBuf<float> K3, dcost;
@@ -746,33 +767,42 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     return fail("allocation");
   S.ids = ids3.p;
   S.K3 = K3.p;
+  S.pt = &pt;
   hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return false; }
+  BVH_DEV(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
   S.st = st;
-  g_pt.st = st;
+  pt.st = st;
   struct StreamGuard {
     hipStream_t s;
     ~StreamGuard() { (void)hipStreamDestroy(s); }
   } sg{st};
   std::vector<uint32_t> iota(n);
   for (uint32_t t = 0; t < n; ++t) iota[t] = t;
-  if (hipMemcpyAsync(dv.p, vpos4, (size_t)nverts * 16, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(didx.p, idx, (size_t)nidx * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
-    err = "upload";
-    return false;
-  }
+  BVH_DEV(hipMemcpyAsync(dv.p, vpos4, (size_t)nverts * 16, hipMemcpyHostToDevice, st), "upload");
+  BVH_DEV(hipMemcpyAsync(didx.p, idx, (size_t)nidx * 4, hipMemcpyHostToDevice, st), "upload");
+  BVH_DEV(hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st), "upload");
   k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p);
+  BVH_DEV(hipGetLastError(), "triangle boxes");
 
   std::vector<BvhHostNode> H(1);
   std::vector<Open> open;
   open.push_back(Open{0, 0, 3 * n, {{0u, 3 * n}}, {}, 0});
-  std::vector<Task> ranges;   // child ranges (triangle units) for the final boxes
+  // child ranges (triangle units) and their boxes: a node's child boxes are
+  // computed in the stage that completes the node, over the triangle order at
+  // that point (calc_bbox at creation, triangles_raytracing.cpp:199), before
+  // the children's own sorts reorder their ranges (first-kept among equal
+  // bounds, so -0.0 / +0.0 come out as the reference's sequential min / max)
+  std::vector<Task> ranges;
   std::vector<std::pair<int32_t, int>> range_of;  // (node, child slot) per range
-  g_pt.start();
-  g_pt.stop(7);  // allocation + upload
+  const size_t max_ranges = 2 * (size_t)n + 8;    // every node but the root is a child range
+  ranges.reserve(max_ranges);
+  DBuf<Task> dranges;
+  if (dranges.reserve(max_ranges) || boxes.reserve(max_ranges)) return fail("allocation");
+  pt.start();
+  pt.stop(7);  // allocation + upload
   while (!open.empty()) {
-    ++g_pt.stages;
+    ++pt.stages;
+    const size_t r0 = ranges.size();
     // this stage: every queued candidate of every open node that tryDivide sorts (> 8 triangles)
     std::vector<Task> tasks;
     std::vector<std::vector<int>> task_of(open.size());
@@ -788,10 +818,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     if (T) {
       if (dtasks.reserve(T) || dcost.reserve(3 * (size_t)T) || ddiv.reserve(3 * (size_t)T) || dact.reserve(T))
         return fail("allocation");
-      if (hipMemcpyAsync(dtasks.p, tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st) != hipSuccess) {
-        err = "upload";
-        return false;
-      }
+      BVH_DEV(hipMemcpyAsync(dtasks.p, tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st), "upload");
       k_stage_copy<<<T, 256, 0, st>>>(dtasks.p, ids3.p, backup.p, n);
       std::vector<Seg> segs;
       segs.reserve(3 * (size_t)T);
@@ -799,16 +826,13 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
         for (const Task &tk : tasks)
           segs.push_back(Seg{a * n + tk.s, a * n + tk.e, 2 * lg2(tk.e - tk.s), 0});
       if (S.sort(segs)) return fail("sort");
-      g_pt.start();
+      pt.start();
       k_sah<<<3 * T, kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, n, rightB3.p, dcost.p, ddiv.p);
-      g_pt.stop(2);
-      if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(cost.data(), dcost.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipMemcpyAsync(dvd.data(), ddiv.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess) {
-        err = "SAH sweep";
-        return false;
-      }
+      pt.stop(2);
+      BVH_DEV(hipGetLastError(), "SAH sweep");
+      BVH_DEV(hipMemcpyAsync(cost.data(), dcost.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
+      BVH_DEV(hipMemcpyAsync(dvd.data(), ddiv.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
+      BVH_DEV(hipStreamSynchronize(st), "SAH sweep");
     }
     // createNode's FIFO, candidate by candidate (triangles_raytracing.cpp:162-173)
     std::vector<Open> next;
@@ -887,60 +911,59 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       H[N.node] = node;
     }
     if (T) {
-      if (hipMemcpyAsync(dact.p, action.data(), T * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
-        err = "upload";
-        return false;
-      }
+      BVH_DEV(hipMemcpyAsync(dact.p, action.data(), T * 4, hipMemcpyHostToDevice, st), "upload");
       k_stage_apply<<<T, 256, 0, st>>>(dtasks.p, dact.p, ids3.p, backup.p, n);
-      if (hipGetLastError() != hipSuccess) { err = "stage apply"; return false; }
+      BVH_DEV(hipGetLastError(), "stage apply");
+    }
+    if (ranges.size() > r0) {  // boxes of the children of the nodes completed in this stage
+      if (ranges.size() > max_ranges) return hfail("child range bound", hipErrorInvalidValue);
+      const size_t nr = ranges.size() - r0;
+      BVH_DEV(hipMemcpyAsync(dranges.p + r0, ranges.data() + r0, nr * sizeof(Task), hipMemcpyHostToDevice, st),
+              "upload");
+      k_range_box<<<(uint32_t)nr, kSahT, 0, st>>>(dranges.p + r0, ids3.p, tbox.p, boxes.p + r0);
+      BVH_DEV(hipGetLastError(), "child boxes");
     }
     open.swap(next);
   }
-  // child boxes over the final triangle order, and the order itself
+  // the child boxes, and the final triangle order
   std::vector<uint32_t> cur(n);
   if (!ranges.empty()) {
-    if (dtasks.reserve(ranges.size()) || boxes.reserve(ranges.size())) return fail("allocation");
     std::vector<TBox> hb(ranges.size());
-    if (hipMemcpyAsync(dtasks.p, ranges.data(), ranges.size() * sizeof(Task), hipMemcpyHostToDevice, st) !=
-        hipSuccess) {
-      err = "upload";
-      return false;
-    }
-    k_range_box<<<(uint32_t)ranges.size(), kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, boxes.p);
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(hb.data(), boxes.p, hb.size() * sizeof(TBox), hipMemcpyDeviceToHost, st) != hipSuccess) {
-      err = "child boxes";
-      return false;
-    }
-    if (hipStreamSynchronize(st) != hipSuccess) { err = "child boxes"; return false; }
+    BVH_DEV(hipMemcpyAsync(hb.data(), boxes.p, hb.size() * sizeof(TBox), hipMemcpyDeviceToHost, st), "child boxes");
+    BVH_DEV(hipStreamSynchronize(st), "child boxes");
     for (size_t r = 0; r < ranges.size(); ++r) {
       BvhBox &b = H[range_of[r].first].box[range_of[r].second];
       std::memcpy(b.mn, hb[r].mn, 12);
       std::memcpy(b.mx, hb[r].mx, 12);
     }
   }
-  if (hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
-    err = "download";
-    return false;
-  }
-  g_pt.start();
+  BVH_DEV(hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st), "download");
+  BVH_DEV(hipStreamSynchronize(st), "download");
+  pt.start();
   bvh_layout(vpos4, idx, nidx, H, cur, out, with_canon);
-  g_pt.stop(3);
-  if (g_pt.on)
+  pt.stop(3);
+  if (pt.on)
     std::fprintf(stderr,
                  "[bvh gpu] %u tris: total %.1f ms | alloc+upload %.1f, partition rounds %.1f (%d rounds), serial "
                  "sorts %.1f (%d launches), SAH %.1f, layout %.1f; %d stages\n",
                  n, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(),
-                 g_pt.acc[7], g_pt.acc[0], g_pt.rounds, g_pt.acc[1], g_pt.serial_launches, g_pt.acc[2], g_pt.acc[3],
-                 g_pt.stages);
+                 pt.acc[7], pt.acc[0], pt.rounds, pt.acc[1], pt.serial_launches, pt.acc[2], pt.acc[3],
+                 pt.stages);
   return true;
+#undef BVH_DEV
 }
 
 }  // namespace rth
 
 // ---- diagnostics (not part of include/rtamd.h) ------------------------------
 extern "C" {
+
+// Fault injection for the builder fallback test: the next `n` device builds
+// fail with a device error before touching the GPU.
+int rtx_bvh_inject_failure(int32_t n) {
+  g_inject_fail.store(n < 0 ? 0 : n);
+  return RT_OK;
+}
 
 // The device sort against libstdc++ std::sort (host_introsort) on n keys:
 // ids[] receives the device permutation; returns RT_OK and *mismatch = number

@@ -1438,6 +1438,10 @@ namespace {
 int g_bvh_mode = RT_BVH_AUTO;
 constexpr int64_t kBvhDeviceMinTris = 32768;  // auto: the device builder from this many triangles
 
+// which builder produced this thread's last tree (rtx_bvh_last_builder):
+// 1 host, 2 device, 3 host after a failed device build (AUTO)
+thread_local int t_bvh_last = 0;
+
 int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, rth::BVHGpu &b,
               bool with_canon) {
   std::string err;
@@ -1445,12 +1449,23 @@ int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t n
   const bool dev = g_bvh_mode == RT_BVH_DEVICE ||
                    (g_bvh_mode == RT_BVH_AUTO && nidx / 3 >= kBvhDeviceMinTris &&
                     hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0);
+  bool fell_back = false;
   if (dev) {
-    if (!rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err, with_canon))
-      return set_err(err.rfind("GPU BVH build", 0) == 0 ? RT_E_DEVICE : RT_E_INVALID, err);
-    return RT_OK;
+    if (rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err, with_canon)) {
+      t_bvh_last = 2;
+      return RT_OK;
+    }
+    const bool device_failure = err.rfind("GPU BVH build", 0) == 0;
+    if (!device_failure) return set_err(RT_E_INVALID, err);
+    if (g_bvh_mode == RT_BVH_DEVICE) return set_err(RT_E_DEVICE, err);
+    // AUTO: the host builder gives the identical tree
+    (void)hipGetLastError();
+    std::fprintf(stderr, "rtamd: %s; building the BVH on the host instead\n", err.c_str());
+    fell_back = true;
+    err.clear();
   }
   if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err, with_canon)) return set_err(RT_E_INVALID, err);
+  t_bvh_last = fell_back ? 3 : 1;
   return RT_OK;
 }
 
@@ -2085,6 +2100,10 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // Diagnostic: persistent launches from now on write per-wave stamps (see
 // PersistQ::stamps) into the device buffer d_buf of cap_waves x 8 u64
 // (d_buf = NULL turns it off). Not part of include/rtamd.h.
+// Builder of this thread's last BVH: 1 host, 2 device, 3 host after a failed
+// device build (AUTO mode falls back; see rtx_bvh_inject_failure)
+int rtx_bvh_last_builder(void) { return t_bvh_last; }
+
 int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
   g_persist_stamps = (unsigned long long *)d_buf;
   g_persist_stamps_cap = d_buf ? cap_waves : 0;
