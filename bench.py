@@ -2,55 +2,60 @@
 """bench.py -- primary-ray throughput of the MI355X renderer (BASELINE.json metric).
 
 Metric: "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355X".
-Workload (N=1 and N>1): BASELINE configs[1], stanford-bunny.obj triangles at
-1920x1080, primary rays (Normal shading, no ground plane: one ray per pixel,
-the pure intersection hot path), over a deterministic 64-frame camera orbit
-(SURVEY.md 8(d)). A "step" is one frame. Orbit frames are independent: up to
---group (8) of them go out in ONE launch (the persistent kernel pulls 8x8 pixel
-tiles of all of them from one work queue), and launches alternate over
---streams (2) HIP streams with their own framebuffers. value = rays of all K
-frames / wall time of the K frames.
+A "step" is one frame of a deterministic 64-frame camera orbit.
+`--workload` picks the headline (default `bunny`: BASELINE configs[1],
+stanford-bunny.obj at 1920x1080, primary rays = Normal shading, no ground plane,
+one ray per pixel, the pure intersection hot path); every key of WORKLOADS
+works at every N, e.g. `--workload mesh_large` is configs[4] (the 1.1 M-triangle
+stand-in at 3840x2160) and `--workload grid` configs[2] (the 256^3 stand-in).
+Orbit frames are independent: up to --group (8) of them go out in ONE launch
+(the persistent kernel pulls 8x8 pixel tiles of all of them from one work
+queue) and launches alternate over --streams (2) HIP streams with their own
+framebuffers. value = rays of all K frames / wall time of the K frames.
 
-Warm-up: every stream gets at least one full launch (and its work-queue state
-via rt_stream_prepare) before t0, whatever --warmup is, so nothing is
-allocated or first-used inside the timed region. The K timed frames are split
-into ceil(K / group) launches of near-equal size.
+Warm-up: every stream gets its work-queue state (rt_stream_prepare) and at
+least one full launch before t0, whatever --warmup is. The K timed frames are
+ceil(K / group) launches of near-equal size, bracketed by synchronize().
 
 At N=1 the other BASELINE configs are measured the same way under "extra"
-(rank 0): the SDF grid (configs[2]; 256^3 GPU-generated stand-in and the
-shipped 65^3), the octree (configs[3]; depth-8 stand-in and shipped sdf_6, both
-3840x2160), the config-5 mesh stand-in (1.1 M triangles, 3840x2160, one GPU)
-and the reference's DEFAULT shading mode on the bunny (plane + Lambert +
-shadows + reflections), reported as primary rays/s and as traced rays/s
-(primary + shadow + reflection rays, counted by the diagnostic kernel).
+(rank 0): the grid (configs[2]: 256^3 stand-in and the shipped 65^3), the
+octree (configs[3]: depth-8 stand-in and the shipped sdf_6, both 3840x2160),
+configs[4]'s mesh on one GPU, and the bunny in the reference's DEFAULT shading
+mode (plane + Lambert + shadows + reflections; also reported as traced rays/s).
 
-Roofline (per workload): achieved = ALGORITHMIC bytes per launch (SURVEY 8(d)
-byte model on the reference's data layout, counted exactly by the diagnostic
-variant of the same kernel over the same frames) / the render kernel's launch
-duration (HIP events on the launch's own stream; frame-weighted, so a short
-last launch does not inflate it), against the 8 TB/s HBM peak. These bytes are
-served mostly by L1/L2 (every scene is cache-resident), so beside it:
-measured DRAM bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc
-passes, MI355X_MICROARCH.md's gfx950 correction), the VALU issue fraction
-(SQ_INSTS_VALU x 2 cycles per wave64 instruction on SIMD-32 / (1024 SIMDs x
-2.4 GHz x duration); the 4-cycle single-wave form beside it) and the L2 hit
-rate. "binding" names the largest of those fractions.
+Roofline (every workload): achieved = ALGORITHMIC bytes per frame (the SURVEY
+8(d) byte model on the reference's data layout, counted exactly by the
+diagnostic variant of the same kernel over the same frames) / ms_per_step (the
+wall time per frame of the timed region, the same clock as `value`). The bytes
+are cache-served (every scene is cache-resident): when they arrive faster than
+the 8 TB/s HBM peak they are held against the aggregate L2 peak instead
+(peak_kind). Measured DRAM bytes per frame (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE,
+separate --pmc passes, MI355X_MICROARCH.md's gfx950 correction) over the same
+wall time give dram.frac; SQ_INSTS_VALU x 2 cycles over 1024 SIMDs x 2.4 GHz
+give valu_frac; SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) the lane
+utilisation. `one_stream` repeats the launches on ONE stream, where a launch's
+HIP-event duration is its own (rocprofv3's average for the kernel must agree).
+Raw counters go to the --detail file, not the JSON line.
 
 Multi-GPU (torch.distributed.run, one process per GPU; rtamd.rowsplit): every
-frame is split into --band-rows (8) row bands dealt round-robin to the ranks,
-with the same launches. Exchange p2p (default): each rank's kernel stores its
-HIT pixels straight into rank 0's frame slots over xGMI (IPC-mapped) and one
-4-byte RCCL all-reduce per group signals completion; exchange gather: one RCCL
-gather per group of packed bands + a de-interleave on rank 0. Total work per
-step is one 1080p frame whatever N is ("strong"); value = pixels of all frames /
-max-over-ranks wall time. Every rank reports its own render-kernel time per
-launch (rank_kernel_ms; the max over ranks bounds the scaling). rank 0 checks
-that its last assembled frame equals a whole-frame render.
+frame is split into --band-rows (8) row bands dealt round-robin to the ranks.
+Exchange p2p (default): each rank's kernel stores its HIT pixels straight into
+rank 0's frame slots over xGMI (IPC-mapped) and one 4-byte RCCL all-reduce per
+group signals completion; exchange gather: one RCCL gather per group of packed
+bands + a de-interleave on rank 0. The frame is fixed as N grows ("strong");
+value = pixels of all frames / max-over-ranks wall time. Every rank reports
+its render-kernel time (rank_kernel_ms). rank 0 checks that its last assembled
+frame equals a whole-frame render.
+
+drop_in (N=1): rt_render, the Renderer::draw surface INTEGRATION.md binds, on
+HOST buffers (upload when not cleared, render, download), ms per frame with the
+copies, on pageable and on pinned (rt_host_pin) buffers.
 
 cpu_baseline: the oracle (C++ restatement of the reference's CPU path, ISPC
-kernels as scalar C++) on every CPU this process is granted (the smallest of
-the affinity set, the cgroup quota and OMP_NUM_THREADS; see host_threads),
-OpenMP schedule(dynamic) over rows, rank 0 at N=1 only.
+kernels as scalar C++) on every CPU this process is granted (see
+host_threads), OpenMP schedule(dynamic) over rows, rank 0 at N=1 only: the
+headline workload, its default shading mode, the shipped 65^3 grid (1080p) and
+sdf_6 (4K), each a time-bounded sample of the same orbit.
 """
 from __future__ import annotations
 
@@ -72,24 +77,40 @@ import rtamd  # noqa: E402
 from rtamd import workloads as WL  # noqa: E402
 
 METRIC = "Mrays/sec + ms/frame at 1920x1080, bunny tris & SDF grid, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-L2_PEAK_GBS = 34500.0  # aggregate L2 (MI355X_MICROARCH.md, L2 per XCD)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+L2_PEAK_GBS = 34500.0  # aggregate L2, 8 XCDs x 4 MiB (MI355X_MICROARCH.md, L2)
 SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock
-W_IMG, H_IMG = 1920, 1080
 
-# key -> (input, W, H, mode, description); the headline is "bunny"
+# key -> (input, W, H, mode, BASELINE config, description)
 WORKLOADS = {
-    "bunny": ("stanford-bunny.obj", 1920, 1080, "primary", "shipped stanford-bunny.obj (69,451 triangles)"),
-    "grid": ("grid", 1920, 1080, "primary", WL.STANDINS["grid"]),
-    "grid_shipped": ("example_grid.grid", 1920, 1080, "primary", "shipped example_grid.grid (65^3)"),
-    "octree": ("octree", 3840, 2160, "primary", WL.STANDINS["octree"]),
-    "octree_shipped": ("sdf_6.octree", 3840, 2160, "primary", "shipped sdf_6.octree (depth 6)"),
-    "mesh_large": ("mesh_large", 3840, 2160, "primary", WL.STANDINS["mesh_large"] + ", 1 GPU"),
-    "default_mode": ("stanford-bunny.obj", 1920, 1080, "default",
+    "bunny": ("stanford-bunny.obj", 1920, 1080, "primary", "configs[1]",
+              "shipped stanford-bunny.obj (69,451 triangles)"),
+    "grid": ("grid", 1920, 1080, "primary", "configs[2]", WL.STANDINS["grid"]),
+    "grid_shipped": ("example_grid.grid", 1920, 1080, "primary", "configs[2] (shipped file)",
+                     "shipped example_grid.grid (65^3)"),
+    "octree": ("octree", 3840, 2160, "primary", "configs[3]", WL.STANDINS["octree"]),
+    "octree_shipped": ("sdf_6.octree", 3840, 2160, "primary", "configs[3] (shipped file)",
+                       "shipped sdf_6.octree (depth 6)"),
+    "mesh_large": ("mesh_large", 3840, 2160, "primary", "configs[4]", WL.STANDINS["mesh_large"]),
+    "default_mode": ("stanford-bunny.obj", 1920, 1080, "default", "configs[1], default shading",
                      "stanford-bunny.obj, the reference's default shading: ground plane + Lambert + shadows + "
                      "one reflection (raytracing.cpp:13-65)"),
 }
 EXTRAS = ["grid", "grid_shipped", "octree", "octree_shipped", "mesh_large", "default_mode"]
+# CPU baselines beside the GPU figures: (workload key, share of --cpu-seconds, max frames)
+CPU_SAMPLES = [("default_mode", 0.25, 16), ("grid_shipped", 0.25, 16), ("octree_shipped", 0.25, 8)]
+
+
+def workload_entry(name):
+    """A WORKLOADS key, or a shipped input file name (1920x1080 primary rays)."""
+    if name in WORKLOADS:
+        return name, WORKLOADS[name]
+    for k, v in WORKLOADS.items():
+        if v[0] == name and v[3] == "primary":
+            return k, v
+    if name.endswith((".obj", ".grid", ".octree")):
+        return name, (name, 1920, 1080, "primary", "shipped input", f"shipped {name}")
+    raise SystemExit(f"unknown --workload {name!r}; keys: {', '.join(WORKLOADS)} or a shipped input file")
 
 
 def parse():
@@ -97,7 +118,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--workload", default="stanford-bunny.obj")
+    ap.add_argument("--workload", default="bunny", help="a WORKLOADS key or a shipped input file")
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
                     help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
@@ -107,8 +128,11 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the launches alternate over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="wall budget of the CPU sample")
+    ap.add_argument("--no-drop-in", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="wall budget of all CPU samples")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the raw counters and per-launch times (not the JSON line)")
     ap.add_argument("--dist", action="store_true",
                     help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
@@ -149,7 +173,7 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def orbit_params(n, W=W_IMG, H=H_IMG, mode="primary"):
+def orbit_params(n, W, H, mode="primary"):
     orbit = WL.orbit_positions(64)
     sm = rtamd.ShadingMode.Normal if mode == "primary" else rtamd.ShadingMode.Lambert
     return [WL.params_for(orbit[k % 64], W, H, sm) for k in range(n)]
@@ -177,15 +201,14 @@ def stream_pool(k):
     reused by every measurement. Streams share the device's hardware queues
     (GPU_MAX_HW_QUEUES, 4 here) round-robin in creation order; a stream created
     per measurement would sooner or later share a queue with the other one and
-    serialise the 'overlapping' launches (seen as every 4th rank of
-    tools/ab.py split running at one-stream speed). Four consecutive pool
-    streams, never the null stream."""
+    serialise the 'overlapping' launches. Four consecutive pool streams, never
+    the null stream."""
     while len(_POOL) < max(k, 4):
         _POOL.append(torch.cuda.Stream())
     return _POOL[:k]
 
 
-def run_single(scene, params, warmup, steps, W=W_IMG, H=H_IMG, inflight=2, tile=None, batch=1):
+def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=1):
     """Full frames (or one rank's row bands with `tile`), render kernel only.
     Frames go out in launches of up to `batch` frames (rt_render_device_frames);
     launch j is issued on stream j % inflight with its own framebuffers. Before
@@ -237,7 +260,7 @@ def per_frame_ms(launches):
     return sum(ms for ms, _ in launches) / sum(n for _, n in launches)
 
 
-def run_distributed(scene, params, warmup, steps, a):
+def run_distributed(scene, params, warmup, steps, a, W, H):
     """N>1: row bands per rank, assembled on rank 0 (rtamd.rowsplit). With the
     p2p exchange every rank stores its hit pixels straight into rank 0's frame
     over xGMI and one 4-byte RCCL all-reduce per group of frames signals
@@ -248,7 +271,7 @@ def run_distributed(scene, params, warmup, steps, a):
     from rtamd.rowsplit import RowSplitRenderer
 
     def make(exchange):
-        r = RowSplitRenderer(scene, W_IMG, H_IMG, band_rows=a.band_rows, group=a.group, depth=a.depth,
+        r = RowSplitRenderer(scene, W, H, band_rows=a.band_rows, group=a.group, depth=a.depth,
                              streams=a.streams, exchange=exchange)
         # warm every stream and slot group the timed region will use
         r.render(params[:max(warmup, a.group * a.streams * a.depth)])
@@ -262,7 +285,7 @@ def run_distributed(scene, params, warmup, steps, a):
     ok = 1
     nw = max(warmup, a.group * a.streams * a.depth)
     if dist.get_rank() == 0:
-        _, _, (c1, t1) = run_single(scene, params[nw - 1:nw], 0, 1, inflight=1)
+        _, _, (c1, t1) = run_single(scene, params[nw - 1:nw], 0, 1, W, H, inflight=1)
         fc, ft = rs.last()
         ok = int(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
     if not rs._all_ok(ok):
@@ -283,44 +306,78 @@ def run_distributed(scene, params, warmup, steps, a):
     # render-launch duration of this rank's bands: the same launches (a.group frames each,
     # a.streams streams) rendered locally, HIP events on each launch's stream
     n = min(steps, 64)
-    _, launches, _ = run_single(scene, params[warmup:warmup + n], 0, n, inflight=a.streams, tile=rs.tile,
+    _, launches, _ = run_single(scene, params[warmup:warmup + n], 0, n, W, H, inflight=a.streams, tile=rs.tile,
                                 batch=a.group)
-    return wall, per_frame_ms(launches) * a.group, rs
+    return wall, per_frame_ms(launches), rs
 
 
-def roofline(scene, params, tile, kms, frames_per_launch, W=W_IMG, H=H_IMG):
-    """algorithmic bytes per launch (counted exactly by the
-    diagnostic kernel over the same frames) / the event-timed launch duration,
-    against the HBM peak. The PMC-measured fields are added by attach_pmc()."""
-    c = scene.count_work(params, W, H, clear=True, tile=tile)
-    npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
-    algo = scene.algorithmic_bytes(c, npx * len(params)) / len(params) * frames_per_launch
-    achieved = algo / (kms * 1e-3) / 1e9
-    per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
-    peak, kind = peak_for(achieved)
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "peak_kind": kind, "unit": "GB/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
-            "basis": "algorithmic bytes (SURVEY.md 8(d) byte model on the reference's data layout); "
-                     "the scenes are cache-resident, so these bytes are served mostly by L1/L2, not DRAM",
-            "algorithmic_bytes_per_launch": int(algo), "kernel_ms": round(kms, 5),
-            "frames_per_launch": frames_per_launch, "work_per_ray": per_ray,
-            "algorithmic_vs_l2_peak": round(achieved / L2_PEAK_GBS, 4)}
-
-
+# ------------------------------------------------------------ roofline --
 def peak_for(achieved):
     """The HBM peak, unless the algorithmic bytes arrive faster than HBM can
     deliver -- then they are cache-served by construction and the aggregate L2
-    peak is the roof they are held against (a fraction above 1 of the HBM peak
-    would say nothing about DRAM)."""
+    peak is the roof they are held against."""
     if achieved <= HBM_PEAK_GBS:
         return HBM_PEAK_GBS, "hbm"
-    return L2_PEAK_GBS, "l2 (algorithmic bytes above the 8 TB/s HBM peak: cache-served)"
+    return L2_PEAK_GBS, "l2"
 
 
-def one_stream_roof(algo_bytes, kms):
-    a = algo_bytes / (kms * 1e-3) / 1e9
+def work_model(scene, params, tile, W, H):
+    """algorithmic bytes per frame, from the diagnostic kernel's
+    exact work counts over the same frames. -> (bytes per frame, work per ray)."""
+    c = scene.count_work(params, W, H, clear=True, tile=tile)
+    npx = (rtamd.lib().rt_tile_pixels(W, H, ctypes.byref(tile)) if tile is not None else W * H)
+    per_frame = scene.algorithmic_bytes(c, npx * len(params)) / len(params)
+    per_ray = {k: round(v / (npx * len(params)), 4) for k, v in c.items() if v}
+    return per_frame, per_ray
+
+
+def roofline(algo_frame, ms_step, ctr=None, pmc_err=None, group=8):
+    """The contract's roofline object for one workload, on the wall clock:
+    achieved = algorithmic bytes per frame / ms_per_step; frac x peak x
+    ms_per_step reproduces the bytes per frame. PMC counters (per launch of
+    `group` frames, one stream) give the measured DRAM traffic and issue
+    fractions over the same wall time."""
+    dur = ms_step * 1e-3
+    achieved = algo_frame / dur / 1e9
+    peak, kind = peak_for(achieved)
+    rl = {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "peak_kind": kind, "unit": "GB/s",
+          "frac": round(achieved / peak, 4), "traffic": None, "per": "frame (step); time = ms_per_step",
+          "algorithmic_bytes_per_frame": int(algo_frame), "ms_per_step": round(ms_step, 5),
+          "hbm_frac_of_algorithmic": round(achieved / HBM_PEAK_GBS, 4)}
+    if pmc_err or not ctr or "FETCH_SIZE" not in ctr or "SQ_INSTS_VALU" not in ctr:
+        rl["pmc_error"] = (pmc_err or "no counters")[:160]
+        return rl
+    fetch = 2.0 * ctr["FETCH_SIZE"] * 1024.0 / group  # gfx950: FETCH_SIZE reports half; KiB -> B; per frame
+    write = ctr["WRITE_SIZE"] * 1024.0 / group
+    rl["traffic"] = round(fetch + write)
+    dram = (fetch + write) / dur / 1e9
+    valu = ctr["SQ_INSTS_VALU"] / group
+    issue = valu * 2.0 / (SIMDS * CLOCK_HZ * dur)
+    lane = (ctr["SQ_THREAD_CYCLES_VALU"] / (64.0 * ctr["SQ_ACTIVE_INST_VALU"])
+            if ctr.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in ctr else None)
+    hits, miss = ctr.get("TCC_HIT_sum", 0.0), ctr.get("TCC_MISS_sum", 0.0)
+    rl["dram"] = {"achieved": round(dram, 1), "frac": round(dram / HBM_PEAK_GBS, 4),
+                  "write_bytes_per_frame": round(write)}
+    rl["valu_frac"] = round(issue, 4)
+    rl["lane_util"] = round(lane, 4) if lane is not None else None
+    rl["l2_hit"] = round(hits / (hits + miss), 4) if hits + miss else None
+    roofs = {"dram": dram / HBM_PEAK_GBS, "valu_issue": issue, "cache_bytes": achieved / L2_PEAK_GBS}
+    top = max(roofs, key=roofs.get)
+    rl["binding"] = top if roofs[top] >= 0.5 else f"latency (largest roof {top} {roofs[top]:.2f})"
+    return rl
+
+
+def one_stream_leg(scene, params, warmup, steps, W, H, group, algo_frame):
+    """The same launches on ONE stream: a launch's HIP-event duration is its own
+    (the figure rocprofv3's kernel trace must reproduce)."""
+    w1, l1, _ = run_single(scene, params, warmup, steps, W, H, inflight=1, batch=group)
+    kl = statistics.mean(ms for ms, n in l1 if n == group) if any(n == group for _, n in l1) else \
+        per_frame_ms(l1) * group
+    kf = per_frame_ms(l1)
+    a = algo_frame / (kf * 1e-3) / 1e9
     peak, kind = peak_for(a)
-    return {"achieved": round(a, 1), "peak": peak, "peak_kind": kind, "frac": round(a / peak, 4)}
+    return {"ms_per_step": round(w1 * 1e3 / steps, 4), "kernel_ms_per_launch": round(kl, 5),
+            "frames_per_launch": group, "achieved": round(a, 1), "peak_kind": kind, "frac": round(a / peak, 4)}
 
 
 # ------------------------------------------------------------ PMC passes --
@@ -328,7 +385,8 @@ PMC_PASSES = [
     ["FETCH_SIZE"],
     ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
     ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU",
-     "SQ_INSTS_VMEM_RD", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "GRBM_GUI_ACTIVE"],
+     "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VMEM_RD", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum",
+     "GRBM_GUI_ACTIVE"],
 ]
 PMC_LAUNCHES = 2
 
@@ -359,7 +417,7 @@ def pmc_counters(keys, group):
                    "--plan", plan, "--group", str(group), "--launches", str(PMC_LAUNCHES)]
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
             if r.returncode != 0:
-                return out, f"pass {ctrs} rc={r.returncode}: {r.stderr[-300:]}"
+                return out, f"pass {ctrs[0]} rc={r.returncode}: {r.stderr[-200:]}"
             rows = {}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
@@ -370,7 +428,7 @@ def pmc_counters(keys, group):
                             float(row["Counter_Value"])
             disp = [rows[k] for k in sorted(rows)]
             if len(disp) != PMC_LAUNCHES * len(keys):
-                return out, f"pass {ctrs}: {len(disp)} render dispatches, expected {PMC_LAUNCHES * len(keys)}"
+                return out, f"pass {ctrs[0]}: {len(disp)} render dispatches, expected {PMC_LAUNCHES * len(keys)}"
             for j, k in enumerate(keys):
                 mine = disp[j * PMC_LAUNCHES:(j + 1) * PMC_LAUNCHES]
                 for c in ctrs:
@@ -380,111 +438,112 @@ def pmc_counters(keys, group):
     return out, None
 
 
-def attach_pmc(rl, ctr, err):
-    """Add the counter-derived roofs to a roofline dict (per launch of the same shape)."""
-    if err or not ctr or "FETCH_SIZE" not in ctr or "SQ_INSTS_VALU" not in ctr:
-        rl["pmc_error"] = err or "no counters"
-        return rl
-    fetch = 2.0 * ctr["FETCH_SIZE"] * 1024.0  # gfx950: FETCH_SIZE reports half of the bytes; KiB -> B
-    write = ctr["WRITE_SIZE"] * 1024.0
-    dur = rl["kernel_ms"] * 1e-3
-    rl["traffic"] = round(fetch + write)
-    dram_gbs = (fetch + write) / dur / 1e9
-    valu = ctr["SQ_INSTS_VALU"]
-    issue2 = valu * 2.0 / (SIMDS * CLOCK_HZ * dur)
-    issue4 = valu * 4.0 / (SIMDS * CLOCK_HZ * dur)
-    hits, miss = ctr.get("TCC_HIT_sum", 0.0), ctr.get("TCC_MISS_sum", 0.0)
-    rl["dram"] = {"fetch_bytes": round(fetch), "write_bytes": round(write), "achieved": round(dram_gbs, 1),
-                  "frac": round(dram_gbs / HBM_PEAK_GBS, 4),
-                  "correction": "FETCH_SIZE x2 (gfx950), KiB -> B"}
-    rl["valu_issue"] = {"insts_per_launch": round(valu), "frac": round(issue2, 4),
-                        "frac_4cyc": round(issue4, 4),
-                        "model": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x 2.4 GHz x "
-                                 "launch duration); frac_4cyc: the single-wave 4-cycle issue cost"}
-    rl["l2"] = {"hit_rate": round(hits / (hits + miss), 4) if hits + miss else None,
-                "tcp_to_tcc_read_req": round(ctr.get("TCP_TCC_READ_REQ_sum", 0.0)),
-                "tcp_accesses": round(ctr.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0))}
-    rl["sq"] = {k: round(ctr[k]) for k in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU",
-                                           "SQ_INSTS_VMEM_RD", "GRBM_GUI_ACTIVE") if k in ctr}
-    roofs = {"dram": rl["dram"]["frac"], "valu_issue": issue2, "algorithmic_vs_l2": rl["algorithmic_vs_l2_peak"]}
-    top = max(roofs, key=roofs.get)
-    rl["binding"] = top if roofs[top] >= 0.5 else \
-        f"latency: no throughput roof above {roofs[top]:.2f} (largest: {top})"
-    return rl
-
-
 # ------------------------------------------------------------ workloads --
-def measure(key, warmup, steps, streams, group, pmc, pmc_err, scene=None):
-    src, W, H, mode, desc = WORKLOADS[key]
-    own = scene is None
-    if own:
-        scene, off = WL.scene_for(src)
-    else:
-        off = None
-    if mode == "default":
-        if off is None:
-            off = WL.load_input(src)[2]
-        scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off))
-    else:
-        scene.set_plane(None)
+def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
+    """One extra workload at N=1: compact figures for the JSON line, the rest in `detail`."""
+    src, W, H, mode, cfg, desc = entry
+    scene, off = WL.scene_for(src)
+    scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
     prm = orbit_params(warmup + steps, W, H, mode)
     wall, launches, _ = run_single(scene, prm, warmup, steps, W, H, inflight=streams, batch=group)
-    kms = per_frame_ms(launches) * group
-    rl = attach_pmc(roofline(scene, prm[warmup:], None, kms, group, W, H), pmc.get(key), pmc_err)
-    amort = [ms / n for ms, n in launches]
-    out = {"workload": f"{desc}, {W}x{H}, {'primary rays (Normal shading, no plane)' if mode == 'primary' else 'default mode'}, "
-                       "same orbit",
-           "value": round(W * H * steps / wall / 1e6, 1), "unit": "Mrays/s",
-           "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
-           "kernel_ms_per_frame": {"mean": round(per_frame_ms(launches), 5),
-                                   "p50": round(statistics.median(amort), 5)},
-           "roofline": rl}
+    ms_step = wall * 1e3 / steps
+    algo, per_ray = work_model(scene, prm[warmup:], None, W, H)
+    rl = roofline(algo, ms_step, pmc.get(key), pmc_err, group)
+    one = one_stream_leg(scene, prm, warmup, steps, W, H, group, algo) if streams > 1 else None
+    out = {"config": cfg, "res": f"{W}x{H}", "mode": mode,
+           "value": round(W * H * steps / wall / 1e6, 1), "ms_per_step": round(ms_step, 4),
+           "frac": rl["frac"], "peak_kind": rl["peak_kind"],
+           "dram_frac": rl.get("dram", {}).get("frac"), "valu_frac": rl.get("valu_frac"),
+           "lane_util": rl.get("lane_util"), "1stream_launch_ms": one["kernel_ms_per_launch"] if one else None}
     if mode == "default":
-        rays = rl["work_per_ray"].get("rays", 1.0)
-        out["traced_rays_per_pixel"] = rays
+        rays = per_ray.get("rays", 1.0)
+        out["traced_rays_per_px"] = rays
         out["traced_value"] = round(W * H * rays * steps / wall / 1e6, 1)
-        out["value_note"] = ("value = primary rays (pixels) per second; traced_value counts every ray the "
-                             "frame traces (primary + shadow + reflection + reflection shadow)")
-    if streams > 1:  # the same launches on ONE stream: a launch's duration is its own
-        w1, l1, _ = run_single(scene, prm, warmup, steps, W, H, inflight=1, batch=group)
-        k1 = per_frame_ms(l1) * group
-        out["one_stream"] = {"ms_per_step": round(w1 * 1e3 / steps, 4), "kernel_ms": round(k1, 5),
-                             **one_stream_roof(rl["algorithmic_bytes_per_launch"], k1)}
-    if own:
-        scene.close()
+    detail[key] = {"workload": desc, "roofline": rl, "one_stream": one, "work_per_ray": per_ray,
+                   "launch_ms": [round(ms, 5) for ms, _ in launches], "pmc_per_launch": pmc.get(key)}
+    scene.close()
     torch.cuda.synchronize()
     return out
 
 
-def cpu_baseline(name, budget_s, mode="primary", max_frames=64):
+def drop_in(scene, params, W, H, frames=16):
+    """rt_render on HOST buffers (Renderer::draw's surface, INTEGRATION.md):
+    ms per frame including the copies, cleared frames (the app's
+    frameBuf.clear() + draw -> RT_FLAG_CLEAR: no upload) and tPrev frames
+    (upload of color and t, then write-on-hit), on pageable and pinned buffers."""
+    import numpy as np
+    L = rtamd.lib()
+    out = {}
+    for pinned in (False, True):
+        c = np.zeros((H, W), np.uint32)
+        t = np.full((H, W), np.inf, np.float32)
+        if pinned:
+            rtamd._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+            rtamd._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+        try:
+            for clear in (True, False):
+                scene.render(params[0], c, t, clear=clear)  # warm
+                t0 = time.perf_counter()
+                ks = [scene.render(params[k % len(params)], c, t, clear=clear) for k in range(frames)]
+                wall = (time.perf_counter() - t0) * 1e3 / frames
+                out[f"{'pinned' if pinned else 'pageable'}_{'clear' if clear else 'tprev'}_ms"] = round(wall, 4)
+                out.setdefault("kernel_ms", round(statistics.median(ks), 4))
+        finally:
+            if pinned:
+                L.rt_host_unpin(c.ctypes.data)
+                L.rt_host_unpin(t.ctypes.data)
+    out["note"] = f"rt_render on host buffers, {W}x{H}, ms/frame incl. copies, {frames} frames each"
+    return out
+
+
+def cpu_scene(src):
+    """The oracle's scene of a workload input (the same arrays the GPU renders)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
     import cpuref  # the oracle: test infrastructure, used here only as the CPU baseline
     from rtamd import data
-    p = data.path(name)
+    if src.endswith(".obj"):
+        v, i = cpuref.load_obj(data.path(src))
+        return cpuref.RefScene.mesh(v, i), float((v[:, 1] / v[:, 3]).min())
+    if src.endswith(".grid"):
+        p = data.path(src)
+        return cpuref.RefScene.grid(np.fromfile(p, np.uint32, 3), np.fromfile(p, np.float32, offset=12)), -1.0
+    if src.endswith(".octree"):
+        return cpuref.RefScene.octree(np.fromfile(data.path(src), np.uint8, offset=4)), -1.0
+    # a stand-in: the arrays the GPU scene is built from
+    bunny = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
+    if src == "mesh_large":
+        m = rtamd.subdivide_mesh(bunny, 2)
+        return cpuref.RefScene.mesh(m.vPos4f, m.indices), float(bunny.vPos4f[:, 1].min())
+    sm = rtamd.SDFMesh(bunny)
+    try:
+        if src == "grid":
+            return cpuref.RefScene.grid(*sm.grid(256)), -1.0
+        return cpuref.RefScene.octree(sm.octree(8)), -1.0
+    finally:
+        sm.close()
+
+
+def cpu_baseline(entry, budget_s, max_frames):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpuref
+    src, W, H, mode, cfg, desc = entry
     threads, why = host_threads()
-    v, i = cpuref.load_obj(p)
-    sc = cpuref.RefScene.mesh(v, i)
-    if mode == "default":
-        sc.set_plane(True, (0.0, 1.0, 0.0), float((v[:, 1] / v[:, 3]).min()))
-    else:
-        sc.set_plane(False)
+    sc, off = cpu_scene(src)
+    sc.set_plane(mode == "default", (0.0, 1.0, 0.0), off)
     orbit = WL.orbit_positions(64)
     frames, ms_total = 0, 0.0
     t0 = time.perf_counter()
-    while frames < max_frames and (time.perf_counter() - t0) < budget_s:
-        vi, pi = cpuref.camera_matrices(orbit[frames % 64], aspect=W_IMG / H_IMG)
+    while frames < max_frames and (frames == 0 or (time.perf_counter() - t0) < budget_s):
+        vi, pi = cpuref.camera_matrices(orbit[frames % 64], aspect=W / H)
         P = cpuref.make_params(orbit[frames % 64], vi, pi, mode=0 if mode == "primary" else 1)
-        _, _, _, ms = sc.render(P, W_IMG, H_IMG, threads=threads)
+        _, _, _, ms = sc.render(P, W, H, threads=threads)
         ms_total += ms
         frames += 1
-    mrays = W_IMG * H_IMG * frames / (ms_total * 1e-3) / 1e6
-    return {"value": round(mrays, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "ms_per_frame": round(ms_total / frames, 2), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-            "threads_from": why,
-            "sample": f"{frames} frames of the 64-frame orbit, {name} {W_IMG}x{H_IMG} "
-                      f"{'primary rays' if mode == 'primary' else 'default mode (plane + Lambert + shadows + reflection)'}, "
-                      f"OpenMP schedule(dynamic) over rows on {threads} threads ({why}), timed "
-                      f"around the pixel loop as Renderer::draw does; ISPC kernels as scalar C++ (oracle/cpuref.cpp)"}
+    return {"value": round(W * H * frames / (ms_total * 1e-3) / 1e6, 2), "unit": "Mrays/s", "cores": threads,
+            "kind": "port", "ms_per_frame": round(ms_total / frames, 2),
+            "sample": f"{frames} orbit frames, {src} {W}x{H} {mode}"}, why
 
 
 def main():
@@ -495,18 +554,19 @@ def main():
     a = parse()
     if not 1 <= a.group <= 8:
         raise SystemExit("--group must be 1..8 (frames per launch)")
+    key, entry = workload_entry(a.workload)
+    src, W, H, mode, cfg, desc = entry
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     use_dist = world > 1 or a.dist
-    headline = "bunny" if a.workload == "stanford-bunny.obj" else None
     pmc, pmc_err = {}, "skipped (--no-pmc or N>1)"
     if not use_dist and not a.no_pmc:
-        keys = ([headline] if headline else []) + ([] if a.no_extra else EXTRAS)
-        if keys:  # child processes, before this one initialises the GPU
-            pmc, pmc_err = pmc_counters(keys, a.group)
+        WORKLOADS.setdefault(key, entry)
+        keys = [key] + ([] if a.no_extra else [k for k in EXTRAS if k != key])
+        pmc, pmc_err = pmc_counters(keys, a.group)  # child processes, before this one initialises the GPU
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
@@ -524,25 +584,23 @@ def main():
             dist.init_process_group(backend)
     rtamd._lib.check(rtamd.lib().rt_set_device(device))
 
-    kind, payload, _ = WL.load_input(a.workload)
-    scene = WL.make_scene(kind, payload)
-    scene.set_plane(None)
-    params = orbit_params(max(a.warmup + a.steps, a.group * a.streams * a.depth))
+    scene, off = WL.scene_for(src)
+    scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
+    params = orbit_params(max(a.warmup + a.steps, a.group * a.streams * a.depth), W, H, mode)
+    detail = {"cmd": " ".join(sys.argv), "headline": key}
 
     latency = None
+    tile = None
     if not use_dist:
-        wall, launches, _ = run_single(scene, params, a.warmup, a.steps, inflight=a.streams, batch=a.group)
-        kms = per_frame_ms(launches) * a.group
-        amort = [ms / n for ms, n in launches]
-        tile = None
+        wall, launches, _ = run_single(scene, params, a.warmup, a.steps, W, H, inflight=a.streams, batch=a.group)
+        detail["headline_launch_ms"] = [round(ms, 5) for ms, _ in launches]
         if a.streams * a.group > 1:  # one frame at a time (latency), reported beside
             nl = min(a.steps, 64)
-            lwall, ll, _ = run_single(scene, params, min(a.warmup, 8), nl, inflight=1)
+            lwall, ll, _ = run_single(scene, params, min(a.warmup, 8), nl, W, H, inflight=1)
             lat = [ms for ms, _ in ll]
-            latency = {"ms_per_frame": round(lwall * 1e3 / nl, 4), "kernel_ms_mean": round(statistics.mean(lat), 5),
-                       "kernel_ms_p50": round(statistics.median(lat), 5), "frames": nl}
+            latency = {"ms_per_frame": round(lwall * 1e3 / nl, 4), "kernel_ms_p50": round(statistics.median(lat), 5)}
     else:
-        wall, kms, rs = run_distributed(scene, params, a.warmup, a.steps, a)
+        wall, kms, rs = run_distributed(scene, params, a.warmup, a.steps, a, W, H)
         tile = rs.tile
         dev_t = "cpu" if dist.get_backend() == "gloo" else "cuda"
         t = torch.tensor([wall], dtype=torch.float64, device=dev_t)
@@ -553,59 +611,75 @@ def main():
         dist.all_reduce(kall, op=dist.ReduceOp.SUM)
         rank_kms = [round(float(x), 5) for x in kall.cpu()]
         if rank == 0:  # the assembled last frame must equal a whole-frame render of it
-            _, _, (c1, t1) = run_single(scene, params[a.warmup + a.steps - 1:a.warmup + a.steps], 0, 1, inflight=1)
+            _, _, (c1, t1) = run_single(scene, params[a.warmup + a.steps - 1:a.warmup + a.steps], 0, 1, W, H,
+                                        inflight=1)
             fc, ft = rs.last()
             check_equal = bool(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
         dist.barrier()
         rs.close()
 
-    rl = roofline(scene, params[a.warmup:a.warmup + a.steps], tile, kms, a.group)
-    if headline and not use_dist:
-        attach_pmc(rl, pmc.get(headline), pmc_err)
-    value = W_IMG * H_IMG * a.steps / wall / 1e6
+    ms_step = wall * 1e3 / a.steps
+    # algorithmic bytes of the WHOLE frame (every rank's bands) over the max-over-ranks wall time
+    algo, per_ray = work_model(scene, params[a.warmup:a.warmup + min(a.steps, 64)], None, W, H)
+    rl = roofline(algo, ms_step, pmc.get(key), pmc_err, a.group)
+    detail["headline_work_per_ray"] = per_ray
+    detail["headline_pmc_per_launch"] = pmc.get(key)
+    value = W * H * a.steps / wall / 1e6
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall * 1e3 / a.steps, 4),
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-        "data": f"synthetic deterministic 64-frame camera orbit over the shipped {a.workload}",
-        "config": {"workload": f"{a.workload} triangles {W_IMG}x{H_IMG} primary rays "
-                               "(BASELINE configs[1]); Normal shading, no plane",
-                   "resolution": [W_IMG, H_IMG], "camera": "orbit r=2.5 h=0.5 fovy 45",
+        "data": f"synthetic deterministic 64-frame camera orbit over {desc}",
+        "config": {"workload": f"{key}: {desc}, {W}x{H}, "
+                               f"{'primary rays (Normal shading, no plane)' if mode == 'primary' else 'default shading'}"
+                               f" (BASELINE {cfg})",
+                   "resolution": [W, H], "camera": "orbit r=2.5 h=0.5 fovy 45",
                    "parallelism": (f"row bands of {a.band_rows} rows x {world} GPUs, exchange "
                                    f"{rs.exchange}, {a.group} frames per launch and signal, {a.streams} streams")
                    if use_dist else "1 GPU, 1 thread per pixel",
                    "frames_per_launch": a.group, "streams": a.streams},
         "roofline": rl,
     }
-    if not use_dist:
-        out["kernel_ms_per_frame"] = {"mean": round(per_frame_ms(launches), 5),
-                                      "p50": round(statistics.median(amort), 5)}
     if latency is not None:
         out["frame_latency"] = latency
     if not use_dist and a.streams > 1:
-        w1, l1, _ = run_single(scene, params, a.warmup, a.steps, inflight=1, batch=a.group)
-        k1 = per_frame_ms(l1) * a.group
-        out["roofline_one_stream"] = {"streams": 1, "ms_per_step": round(w1 * 1e3 / a.steps, 4),
-                                      "kernel_ms": round(k1, 5),
-                                      **one_stream_roof(rl["algorithmic_bytes_per_launch"], k1)}
+        out["roofline"]["one_stream"] = one_stream_leg(scene, params, a.warmup, a.steps, W, H, a.group, algo)
     if use_dist:
-        out["rank_kernel_ms"] = {"per_rank": rank_kms, "max": max(rank_kms),
-                                 "note": "render-kernel ms per launch of this rank's bands "
-                                         f"({a.group} frames, {a.streams} streams); the max bounds the scaling"}
+        out["rank_kernel_ms_per_frame"] = {"per_rank": rank_kms, "max": max(rank_kms)}
     if use_dist and rank == 0:
         out["frame_check"] = {"assembled_equals_single_render": check_equal,
                               "backend": dist.get_backend(), "exchange": rs.exchange,
                               "fallback": getattr(rs, "fallback", None)}
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
+    if rank == 0 and not use_dist and not a.no_drop_in:
+        out["drop_in"] = drop_in(scene, params, W, H)
+    scene.close()
     if rank == 0 and not use_dist and not a.no_extra:
-        out["extra"] = {k: measure(k, min(a.warmup, 16), min(a.steps, 64), a.streams, a.group, pmc, pmc_err)
-                        for k in EXTRAS}
+        out["extra"] = {k: measure(k, WORKLOADS[k], min(a.warmup, 16), min(a.steps, 64), a.streams, a.group, pmc,
+                                   pmc_err, detail)
+                        for k in EXTRAS if k != key}
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
+        share = 1.0 - sum(s for _, s, _ in CPU_SAMPLES) if not a.no_extra else 1.0
+        cb, why = cpu_baseline(entry, a.cpu_seconds * share, 64)
+        cb.update({"nproc": os.cpu_count(), "cpu_model": cpu_model(), "threads_from": why,
+                   "impl": "oracle/cpuref.cpp (ISPC kernels as scalar C++), OpenMP schedule(dynamic) over rows, "
+                           "std::chrono around the pixel loop as Renderer::draw"})
         if not a.no_extra:
-            out["cpu_baseline"]["default_mode"] = cpu_baseline(a.workload, a.cpu_seconds / 3, "default", 16)
+            for k, s, mx in CPU_SAMPLES:
+                if k != key:
+                    cb[k], _ = cpu_baseline(WORKLOADS[k], a.cpu_seconds * s, mx)
+        out["cpu_baseline"] = cb
     if rank == 0:
-        print(json.dumps(out), file=json_out, flush=True)
+        try:
+            os.makedirs(os.path.dirname(a.detail), exist_ok=True)
+            with open(a.detail, "w") as f:
+                json.dump(detail, f, indent=1)
+            out["detail_file"] = os.path.relpath(a.detail, ROOT)
+        except OSError as e:
+            out["detail_file"] = f"not written: {e}"
+        line = json.dumps(out, separators=(",", ":"))
+        print(line, file=json_out, flush=True)
+        print(f"bench line: {len(line)} bytes", file=sys.stderr)
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()

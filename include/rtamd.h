@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 5
+#define RTAMD_ABI_VERSION 6
 
 enum rt_status {
   RT_OK = 0,
@@ -153,6 +153,12 @@ int rt_scene_destroy(rt_scene *s);
  * *ms (optional) receives the kernel time in milliseconds (HIP events). */
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W,
               int32_t H, uint32_t flags, float *ms);
+/* Pin (page-lock) a host framebuffer range for rt_render's DMA copies; the
+ * caller keeps it pinned while it reuses the buffer (the reference app keeps
+ * one FrameBuffer across frames, src/main.cpp:88) and unpins it before freeing
+ * it. Optional: rt_render works on pageable memory too, through staged copies. */
+int rt_host_pin(void *ptr, int64_t bytes);
+int rt_host_unpin(void *ptr);
 /* Same on DEVICE buffers, asynchronously on `stream` (hipStream_t or NULL).
  * With tile != NULL only this rank's bands are rendered, packed (rt_tile). */
 int rt_render_device(rt_scene *s, const rt_render_params *p, uint32_t *d_color, float *d_t,

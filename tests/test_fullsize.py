@@ -1,6 +1,7 @@
-"""Full-size parity for the BASELINE configs the bench times on generated
-stand-ins (configs[2]-[4]: their reference inputs are missing,
-.MISSING_LARGE_BLOBS), at the bench's own resolution and launch shape.
+"""Full-size parity for the BASELINE configs the bench times -- the headline
+(configs[1], the shipped bunny) and the generated stand-ins (configs[2]-[4]:
+their reference inputs are missing, .MISSING_LARGE_BLOBS) -- at the bench's own
+resolution and launch shape.
 
 Each case renders orbit frames through rt_render_device_frames -- the
 persistent multi-frame launch bench.py times -- and compares every frame with
@@ -13,7 +14,11 @@ strided subsample of the full-resolution eye rays through rt_intersect_rays.
   configs[3]: stanford-bunny SDF octree of depth 8, 3840x2160 --
               octree_raytracing.cpp:166-208
   configs[4]: stanford-bunny subdivided twice (1,111,216 triangles),
-              3840x2160 -- triangles_raytracing.cpp:260-335
+              3840x2160 -- triangles_raytracing.cpp:260-335; also split into
+              the 8-row bands of 2 and 8 ranks (the multi-GPU path,
+              raytracing.cpp:80-96) through both exchanges' layouts
+  configs[1]: stanford-bunny.obj, 1920x1080: the headline instantiation
+              (render_persist_kernel<MeshS, 4, false>, 8 frames per launch)
 """
 import functools
 
@@ -26,7 +31,9 @@ import scenes as S
 pytestmark = pytest.mark.gpu
 
 ORBIT_K = (0, 21, 42)  # three cameras of the bench's 64-frame orbit, rendered in one launch
-CASES = {"grid256": (1920, 1080), "octree8": (3840, 2160), "mesh_large": (3840, 2160)}
+# the headline: a full 8-frame launch, as every launch of the bench's 20 timed frames but one
+ORBIT_K_CASE = {"bunny": (0, 8, 16, 24, 32, 40, 48, 56)}
+CASES = {"grid256": (1920, 1080), "octree8": (3840, 2160), "mesh_large": (3840, 2160), "bunny": (1920, 1080)}
 
 
 @functools.lru_cache(maxsize=None)
@@ -34,6 +41,8 @@ def standin(key):
     """-> (kind, payload, plane offset): the same arrays feed both renderers."""
     import rtamd
     v, i = S.inputs("stanford-bunny.obj")[1]
+    if key == "bunny":
+        return "mesh", (v, i), S.inputs("stanford-bunny.obj")[2]
     if key == "mesh_large":
         m = rtamd.subdivide_mesh(rtamd.SimpleMesh(v, i), 2)
         assert m.TrianglesNum() == 1_111_216
@@ -102,9 +111,10 @@ def test_fullsize_primary_frames(gpu, key):
     rs, gs = scenes(key)
     set_plane(key, "primary", rs, gs)
     orbit = orbit_positions(64)
-    pos = [orbit[k] for k in ORBIT_K]
+    ks = ORBIT_K_CASE.get(key, ORBIT_K)
+    pos = [orbit[k] for k in ks]
     got = gpu_batch(gs, key, W, H, "primary", pos)
-    for k, p, g in zip(ORBIT_K, pos, got):
+    for k, p, g in zip(ks, pos, got):
         c, t, _, _ = rs.render(S.params(key, W, H, "primary", p, "ref"), W, H)
         assert_same((c, t), g, f"{key} {W}x{H} orbit {k} primary")
 
@@ -143,3 +153,80 @@ def test_fullsize_primary_ray_hits(gpu, key):
     h = g.hitten
     assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
     assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
+
+
+def band_frames(gs, W, H, mode, positions, world, natural):
+    """Every rank's 8-row bands of len(positions) frames, one
+    rt_render_device_frames launch per rank (the bench's launch per group), as
+    the two exchanges lay them out: natural=True -> hits-only stores at their
+    own rows of ONE cleared frame (the p2p exchange into rank 0's frame);
+    natural=False -> packed per-rank slots, gathered and de-interleaved by
+    rt_untile_device (the RCCL gather exchange)."""
+    import ctypes as C
+
+    import torch
+
+    import rtamd
+    from rtamd import _lib
+    L = rtamd.lib()
+    P = [S.params("mesh_large", W, H, mode, pos, "gpu") for pos in positions]
+    tiles = [rtamd.Tile(8, r, world, 0) for r in range(world)]
+    out = []
+    if natural:
+        frames = [(torch.full((H, W), 77, dtype=torch.int32, device="cuda"),
+                   torch.zeros((H, W), dtype=torch.float32, device="cuda")) for _ in P]
+        for c, t in frames:
+            _lib.check(L.rt_clear_device(C.c_void_p(c.data_ptr()), C.c_void_p(t.data_ptr()), W * H, None))
+        fl = _lib.RT_FLAG_CLEAR | _lib.RT_FLAG_HITS_ONLY | _lib.RT_FLAG_TILE_NATURAL
+        for tl in tiles:
+            gs.render_device_frames(P, [c.data_ptr() for c, _ in frames], [t.data_ptr() for _, t in frames], W, H,
+                                    fl, tile=tl)
+        torch.cuda.synchronize()
+        return [(c.cpu().numpy().view(np.uint32), t.cpu().numpy()) for c, t in frames]
+    per = max(L.rt_tile_pixels(W, H, C.byref(tl)) for tl in tiles)
+    for f in range(len(P)):
+        pc = torch.full((world * per,), 55, dtype=torch.int32, device="cuda")
+        pt = torch.zeros((world * per,), dtype=torch.float32, device="cuda")
+        out.append((pc, pt))
+    for r, tl in enumerate(tiles):
+        gs.render_device_frames(P, [pc.data_ptr() + 4 * r * per for pc, _ in out],
+                                [pt.data_ptr() + 4 * r * per for _, pt in out], W, H, _lib.RT_FLAG_CLEAR, tile=tl)
+    res = []
+    for pc, pt in out:
+        c = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        t = torch.empty((H, W), dtype=torch.float32, device="cuda")
+        _lib.check(L.rt_untile_device(C.c_void_p(pc.data_ptr()), C.c_void_p(pt.data_ptr()), per,
+                                      C.c_void_p(c.data_ptr()), C.c_void_p(t.data_ptr()), W, H,
+                                      C.byref(tiles[0]), None))
+        res.append((c, t))
+    torch.cuda.synchronize()
+    return [(c.cpu().numpy().view(np.uint32), t.cpu().numpy()) for c, t in res]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("mode", ["primary", "default"])
+@pytest.mark.parametrize("natural", [True, False], ids=["p2p_layout", "gather_untile"])
+def test_config5_row_bands_assemble_oracle_frame(gpu, world, mode, natural):
+    """configs[4] itself: the 1,111,216-triangle stand-in at 3840x2160 split into
+    8-row bands over `world` ranks (2 ranks take the persistent work queue, 8
+    the block dispatch), two orbit frames per launch; the assembled frames are
+    bitwise the oracle's Renderer::draw of the whole frame."""
+    from rtamd.workloads import orbit_positions
+    W, H = CASES["mesh_large"]
+    rs, gs = scenes("mesh_large")
+    set_plane("mesh_large", mode, rs, gs)
+    ks = (5, 37)
+    pos = [orbit_positions(64)[k] for k in ks]
+    got = band_frames(gs, W, H, mode, pos, world, natural)
+    for k, p, g in zip(ks, pos, got):
+        c, t, _, _ = _oracle_frame("mesh_large", W, H, mode, k)
+        assert_same((c, t), g, f"mesh_large {W}x{H} orbit {k} {mode}, {world} ranks, "
+                               f"{'natural hits-only' if natural else 'gather + untile'}")
+
+
+@functools.lru_cache(maxsize=8)
+def _oracle_frame(key, W, H, mode, k):
+    from rtamd.workloads import orbit_positions
+    rs, _ = scenes(key)
+    set_plane(key, mode, rs, scenes(key)[1])
+    return rs.render(S.params(key, W, H, mode, orbit_positions(64)[k], "ref"), W, H)

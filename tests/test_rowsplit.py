@@ -129,6 +129,86 @@ def test_batched_launches_repeat_across_streams(gpu, name, W, H):
             assert torch.equal(t.view(torch.int32), ref[k][1].view(torch.int32)), f"launch {rep} frame {k}"
 
 
+@pytest.mark.parametrize("name,W,H", [("stanford-bunny.obj", 240, 136), ("sdf_6.octree", 130, 77)])
+@pytest.mark.parametrize("rank", [0, 1])
+@pytest.mark.parametrize("natural", [False, True])
+def test_two_rank_bands_take_the_work_queue(gpu, name, W, H, rank, natural):
+    """Row bands of at most 2 ranks (band_persist_max) take the persistent
+    work-queue kernel in rt_render_device_frames; single-frame
+    rt_render_device never does. Both must give the same pixels: batched ==
+    per-frame == the untiled full frame at the band's rows (natural layout)
+    or packed (RT_FLAG_TILE_NATURAL off)."""
+    from rtamd import _lib
+    from rtamd import workloads as WL
+    rt = gpu
+    sc = S.gpu_scene(name)
+    sc.set_plane(None)
+    orbit = WL.orbit_positions(64)
+    prm = [WL.params_for(orbit[(9 * k) % 64], W, H, rt.ShadingMode.Normal) for k in range(8)]
+    tile = rt.Tile(8, rank, 2, 0)
+    flags = _lib.RT_FLAG_CLEAR | (_lib.RT_FLAG_TILE_NATURAL if natural else 0)
+    npx = rt.lib().rt_tile_pixels(W, H, C.byref(tile))
+    shape = (H, W) if natural else (npx,)
+    bufs = [(torch.full(shape, 5, dtype=torch.int32, device="cuda"),
+             torch.zeros(shape, dtype=torch.float32, device="cuda")) for _ in prm]
+    sc.render_device_frames(prm, [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs], W, H, flags,
+                            tile=tile)
+    rows = np.array([y for y in range(H) if (y // 8) % 2 == rank])
+    for k, p in enumerate(prm):
+        c = torch.full(shape, 5, dtype=torch.int32, device="cuda")
+        t = torch.zeros(shape, dtype=torch.float32, device="cuda")
+        sc.render_device(p, c.data_ptr(), t.data_ptr(), W, H, clear=True, tile=tile,
+                         flags=_lib.RT_FLAG_TILE_NATURAL if natural else 0)
+        fc = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        ft = torch.empty((H, W), dtype=torch.float32, device="cuda")
+        sc.render_device(p, fc.data_ptr(), ft.data_ptr(), W, H, clear=True)
+        torch.cuda.synchronize()
+        assert torch.equal(c, bufs[k][0]), f"frame {k}: batched != single"
+        assert torch.equal(t.view(torch.int32), bufs[k][1].view(torch.int32)), f"frame {k}: batched != single"
+        bc, bt = bufs[k][0].cpu().numpy(), bufs[k][1].cpu().numpy()
+        fcn, ftn = fc.cpu().numpy(), ft.cpu().numpy()
+        if natural:
+            assert np.array_equal(bc[rows], fcn[rows]) and np.array_equal(bt[rows].view(np.int32),
+                                                                          ftn[rows].view(np.int32))
+            other = np.setdiff1d(np.arange(H), rows)
+            assert (bc[other] == 5).all() and (bt[other] == 0).all(), "rows of the other rank were written"
+        else:
+            assert np.array_equal(bc, fcn[rows].reshape(-1))
+            assert np.array_equal(bt.view(np.int32), ftn[rows].reshape(-1).view(np.int32))
+
+
+def test_drop_in_render_host_buffers(gpu):
+    """rt_render (Renderer::draw on host buffers) with pageable and pinned
+    (rt_host_pin) framebuffers: cleared frames equal the oracle's, and a
+    second draw over a kept frame reads t as tPrev and writes only hits
+    (raytracing.cpp:89-94), exactly as the oracle's draw over the same buffers."""
+    rt = gpu
+    L = rt.lib()
+    name, W, H = "stanford-bunny.obj", 320, 180
+    sc = S.gpu_scene(name)
+    S.set_planes(name, "default", sc)
+    rs = S.ref_scene(name)
+    S.set_planes(name, "default", rs)
+    for pinned in (False, True):
+        c = np.zeros((H, W), np.uint32)
+        t = np.full((H, W), np.inf, np.float32)
+        if pinned:
+            rt._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+            rt._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+        try:
+            sc.render(S.params(name, W, H, "default", (0.0, 0.3, 2.5), "gpu"), c, t, clear=True)
+            rc, rt_, _, _ = rs.render(S.params(name, W, H, "default", (0.0, 0.3, 2.5), "ref"), W, H)
+            assert np.array_equal(c, rc) and np.array_equal(t.view(np.uint32), rt_.view(np.uint32))
+            # second draw from another camera over the kept frame: tPrev semantics
+            sc.render(S.params(name, W, H, "default", (0.7, 0.2, 2.3), "gpu"), c, t, clear=False)
+            rs.render(S.params(name, W, H, "default", (0.7, 0.2, 2.3), "ref"), W, H, color=rc, t=rt_)
+            assert np.array_equal(c, rc) and np.array_equal(t.view(np.uint32), rt_.view(np.uint32))
+        finally:
+            if pinned:
+                L.rt_host_unpin(c.ctypes.data)
+                L.rt_host_unpin(t.ctypes.data)
+
+
 def test_hits_only_needs_clear(gpu):
     from rtamd import _lib
     sc = S.gpu_scene("cube.obj")

@@ -34,7 +34,7 @@ WARM, STEPS = 16, 128
 
 def resolve(name):
     if name in bench.WORKLOADS:
-        src, W, H, mode, _ = bench.WORKLOADS[name]
+        src, W, H, mode = bench.WORKLOADS[name][:4]
     else:
         src, W, H, mode = name, 1920, 1080, "primary"
     sc, off = WL.scene_for(src)

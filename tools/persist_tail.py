@@ -43,7 +43,7 @@ def main():
     names = sys.argv[1:] or ["bunny"]
     buf = torch.zeros(CAP * 8, dtype=torch.int64, device="cuda")
     for name in names:
-        src, W, H, mode, _ = bench.WORKLOADS[name]
+        src, W, H, mode = bench.WORKLOADS[name][:4]
         sc, off = WL.scene_for(src)
         sc.set_plane(None)
         prm = bench.orbit_params(64, W, H)

@@ -945,6 +945,8 @@ struct rt_scene {
   float *d_t = nullptr;
   size_t fb_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t xs[2] = {nullptr, nullptr};  // rt_render: colour / t copy streams (render on xs[0])
+  hipEvent_t xev = nullptr;
   // cost-ordered block schedule (see launch_render): per-block cost of the
   // last frame rendered with sched_grid blocks, and the block order derived
   // from it; sched_on = false renders in plain blockIdx order
@@ -1029,6 +1031,15 @@ int pick_maxd(int depth, int32_t &maxd) {
 int ensure_events(rt_scene *s) {
   if (!s->ev0) HIP_TRY(hipEventCreate(&s->ev0));
   if (!s->ev1) HIP_TRY(hipEventCreate(&s->ev1));
+  return RT_OK;
+}
+
+// rt_render's two copy/render streams (non-blocking: no implicit sync with
+// the null stream) and the event that orders the uploads before the kernel
+int ensure_copy_streams(rt_scene *s) {
+  for (hipStream_t &x : s->xs)
+    if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+  if (!s->xev) HIP_TRY(hipEventCreateWithFlags(&s->xev, hipEventDisableTiming));
   return RT_OK;
 }
 
@@ -1734,6 +1745,9 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->sched_ev) (void)hipEventDestroy(s->sched_ev);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->xev) (void)hipEventDestroy(s->xev);
+  for (hipStream_t x : s->xs)
+    if (x) (void)hipStreamDestroy(x);
   (void)hipSetDevice(prev);
   delete s;
   return RT_OK;
@@ -1858,20 +1872,40 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   if (rc) return rc;
   if (!color || !t) return set_err(RT_E_INVALID, "NULL framebuffer");
   const size_t px = (size_t)W * H;
-  if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s))) return rc;
+  if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s)) || (rc = ensure_copy_streams(s))) return rc;
+  // colour and t move on two streams (two DMA engines; concurrent when the host
+  // buffers are pinned, e.g. by rt_host_pin); a cleared frame (the app's
+  // frameBuf.clear() + draw, RT_FLAG_CLEAR) needs no upload
+  hipStream_t a = s->xs[0], b = s->xs[1];
   if (!(flags & RT_FLAG_CLEAR)) {
-    HIP_TRY(hipMemcpy(s->d_color, color, px * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(s->d_t, t, px * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(s->d_color, color, px * 4, hipMemcpyHostToDevice, a));
+    HIP_TRY(hipMemcpyAsync(s->d_t, t, px * 4, hipMemcpyHostToDevice, b));
+    HIP_TRY(hipEventRecord(s->xev, b));
+    HIP_TRY(hipStreamWaitEvent(a, s->xev, 0));
   }
   FrameArgs fa;
   if ((rc = fill_frame(fa, p, s->d_color, s->d_t, W, H, flags, nullptr))) return rc;
-  HIP_TRY(hipEventRecord(s->ev0, 0));
-  if ((rc = launch_render(s, fa, 0))) return rc;
-  HIP_TRY(hipEventRecord(s->ev1, 0));
-  HIP_TRY(hipMemcpy(color, s->d_color, px * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(t, s->d_t, px * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipEventSynchronize(s->ev1));
+  HIP_TRY(hipEventRecord(s->ev0, a));
+  if ((rc = launch_render(s, fa, a))) return rc;
+  HIP_TRY(hipEventRecord(s->ev1, a));
+  HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
+  HIP_TRY(hipMemcpyAsync(t, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
+  HIP_TRY(hipMemcpyAsync(color, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
+  HIP_TRY(hipStreamSynchronize(a));
+  HIP_TRY(hipStreamSynchronize(b));
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  return RT_OK;
+}
+
+int rt_host_pin(void *ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad host range");
+  HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+  return RT_OK;
+}
+
+int rt_host_unpin(void *ptr) {
+  if (!ptr) return set_err(RT_E_INVALID, "NULL pointer");
+  HIP_TRY(hipHostUnregister(ptr));
   return RT_OK;
 }
 

@@ -80,6 +80,8 @@ _SIGS = {
     "rt_scene_destroy": (C.c_int, [C.c_void_p]),
     "rt_render": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                             C.c_uint32, C.POINTER(C.c_float)]),
+    "rt_host_pin": (C.c_int, [C.c_void_p, C.c_int64]),
+    "rt_host_unpin": (C.c_int, [C.c_void_p]),
     "rt_render_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                    C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "rt_untile_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
