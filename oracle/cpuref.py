@@ -16,11 +16,14 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libcpuref.so")
+# CPUREF_LIB: a variant build of the same source (the sanitizer build of `make sanitize`)
+_LIB_PATH = os.environ.get("CPUREF_LIB") or os.path.join(_HERE, "_build", "libcpuref.so")
 _lib = None
 
 
 def build(force: bool = False) -> str:
+    if os.environ.get("CPUREF_LIB"):
+        return _LIB_PATH
     if force or not os.path.exists(_LIB_PATH):
         subprocess.run(["make", "-C", _HERE, "-s"], check=True)
     return _LIB_PATH

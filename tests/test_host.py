@@ -99,14 +99,18 @@ def test_bvh8_identical_to_reference_builder(rt, ref, name):
 @pytest.mark.parametrize("seed,ntri,mode", [(1, 1, "rand"), (2, 7, "rand"), (3, 9, "rand"), (4, 300, "rand"),
                                             (5, 2000, "rand"), (6, 64, "same"), (7, 500, "grid"),
                                             (8, 100, "flat"), (9, 30000, "grid"), (10, 12000, "same"),
-                                            (11, 40000, "rand")])
+                                            (11, 40000, "rand"), (13, 3000, "signed0"), (14, 40000, "signed0")])
 def test_bvh8_edge_cases(rt, ref, seed, ntri, mode):
     """Tiny meshes (root leaf), duplicate triangles (all SAH keys tie), axis-aligned
     grids of triangles (many equal keys) and flat meshes (zero-area boxes). The
     large cases run the parallel sort (ranges >= 4096 ids) and the concurrent
     axes, whose tie order must equal the serial std::sort's."""
     rng = np.random.default_rng(seed)
-    if mode == "same":
+    if mode == "signed0":  # lattice with -0.0 / +0.0 mixed: child box bounds keep calc_bbox's sign bit
+        g = rng.integers(-2, 3, size=(ntri, 3)).astype(np.float64)
+        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
+        v[(v == 0) & (rng.random(v.shape) < 0.5)] = -0.0
+    elif mode == "same":
         v = np.tile(rng.normal(size=(3, 3)), (ntri, 1))
     elif mode == "grid":
         g = rng.integers(0, 6, size=(ntri, 3)).astype(np.float64)

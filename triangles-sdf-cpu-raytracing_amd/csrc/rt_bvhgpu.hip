@@ -568,8 +568,11 @@ __global__ __launch_bounds__(kSahT) void k_range_box(const Task *ranges, const u
   for (uint32_t t = t0; t < t1; ++t) acc = tb_union(acc, tbox[ids[t]]);
   sm[threadIdx.x] = acc;
   __syncthreads();
-  for (int o = kSahT / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < (uint32_t)o) sm[threadIdx.x] = tb_union(sm[threadIdx.x], sm[threadIdx.x + o]);
+  // pairwise over ADJACENT chunk ranges, the earlier one on the left, so the
+  // union stays the sequential left fold (a strided tree would pair chunk i
+  // with chunk i + kSahT/2 first and keep a later equal bound)
+  for (uint32_t o = 1; o < (uint32_t)kSahT; o <<= 1) {
+    if ((threadIdx.x & (2 * o - 1)) == 0) sm[threadIdx.x] = tb_union(sm[threadIdx.x], sm[threadIdx.x + o]);
     __syncthreads();
   }
   if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
