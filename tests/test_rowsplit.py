@@ -133,7 +133,8 @@ def test_batched_launches_repeat_across_streams(gpu, name, W, H):
 @pytest.mark.parametrize("rank", [0, 1])
 @pytest.mark.parametrize("natural", [False, True])
 def test_two_rank_bands_take_the_work_queue(gpu, name, W, H, rank, natural):
-    """Row bands of at most 2 ranks (band_persist_max) take the persistent
+    """Row bands with enough pixels per frame (band_takes_queue; the threshold
+    is lowered here so these small frames qualify) take the persistent
     work-queue kernel in rt_render_device_frames; single-frame
     rt_render_device never does. Both must give the same pixels: batched ==
     per-frame == the untiled full frame at the band's rows (natural layout)
@@ -151,8 +152,13 @@ def test_two_rank_bands_take_the_work_queue(gpu, name, W, H, rank, natural):
     shape = (H, W) if natural else (npx,)
     bufs = [(torch.full(shape, 5, dtype=torch.int32, device="cuda"),
              torch.zeros(shape, dtype=torch.float32, device="cuda")) for _ in prm]
-    sc.render_device_frames(prm, [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs], W, H, flags,
-                            tile=tile)
+    rt.lib().rtx_set_band_queue_px(C.c_int64(1))
+    try:
+        sc.render_device_frames(prm, [c.data_ptr() for c, _ in bufs], [t.data_ptr() for _, t in bufs], W, H, flags,
+                                tile=tile)
+        torch.cuda.synchronize()
+    finally:
+        rt.lib().rtx_set_band_queue_px(C.c_int64(-1))
     rows = np.array([y for y in range(H) if (y // 8) % 2 == rank])
     for k, p in enumerate(prm):
         c = torch.full(shape, 5, dtype=torch.int32, device="cuda")

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -131,6 +132,9 @@ struct GridS {
     return grid_occluded<kMode>(d, o, dir, tn, tf, cnt);
   }
 };
+// PACK: the traversal carries the node coordinates packed in one register
+// (OctXYZ; trees of depth <= 8, i.e. up to 7 stack slots)
+template <bool PACK>
 struct OctS {
   static constexpr int kFields = kOctFields;
   static constexpr bool kCoop = false;
@@ -141,12 +145,12 @@ struct OctS {
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields> st, CT &cnt) const {
-    return oct_intersect<B>(d, o, dir, tn, tf, st, cnt);
+    return oct_intersect<B, PACK>(d, o, dir, tn, tf, st, cnt);
   }
   template <int B, class CT>
   __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields> st, CT &cnt) const {
-    return oct_occluded<B>(d, o, dir, tn, tf, st, cnt);
+    return oct_occluded<B, PACK>(d, o, dir, tn, tf, st, cnt);
   }
 };
 
@@ -277,8 +281,9 @@ __device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
 
 __device__ __forceinline__ int image_row(int yl, const FrameArgs &fa) {
   if (fa.nranks <= 1) return yl;
-  const int k = yl / fa.band_rows, r = yl - k * fa.band_rows;
-  return (k * fa.nranks + fa.rank) * fa.band_rows + r;
+  // unsigned (yl, band_rows > 0): no sign fix-ups around the division
+  const uint32_t br = (uint32_t)fa.band_rows, k = (uint32_t)yl / br, r = (uint32_t)yl - k * br;
+  return (int)((k * (uint32_t)fa.nranks + (uint32_t)fa.rank) * br + r);
 }
 
 // Renderer::draw (raytracing.cpp:67-102). GENERAL=false is the primary-ray
@@ -332,7 +337,9 @@ __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, c
     // full frame's own row (a peer's frame mapped over xGMI)
     const bool peer = (fa.flags & RT_FLAG_TILE_NATURAL) != 0;
     const int yb = peer ? yo : yl;
-    const size_t idx = active ? (size_t)yb * fa.W + xo : 0;
+    // 32-bit pixel index (check_params caps W*H at 2^31): one register live
+    // across the traversal instead of two
+    const uint32_t idx = active ? (uint32_t)yb * (uint32_t)fa.W + (uint32_t)xo : 0u;
     const bool clear = (fa.flags & RT_FLAG_CLEAR) != 0;
     const bool hits_only = (fa.flags & RT_FLAG_HITS_ONLY) != 0;
     const float tPrev = (clear || !active) ? kInf : fa.t[idx];
@@ -656,15 +663,19 @@ struct OctP {
   template <bool FAST>
   __device__ __forceinline__ int start(f3 o, f3 dir, f3 inv, float tf, Ray &R, float &t, f3 &n) const {
     NoCnt c;
-    uint32_t node;
-    return oct_start<true, FAST>(d, o, dir, inv, 0.01f, tf, R, t, n, node, c);
+    OctHitPt hp;
+    const int s = oct_start<FAST>(d, o, dir, inv, 0.01f, tf, R, t, hp, c);
+    if (s == RAY_HIT) n = oct_normal_at(d, hp, c);
+    return s;
   }
   template <bool FAST>
   __device__ __forceinline__ int run(f3 o, f3 dir, f3 inv, float tf, LdsStack<kBlock, kOctFields> st, Ray &R, int limit,
                                      float &t, f3 &n) const {
     NoCnt c;
-    uint32_t node;
-    return oct_run<kBlock, true, FAST, true>(d, o, dir, inv, 0.01f, tf, st, R, limit, t, n, node, c);
+    OctHitPt hp;
+    const int s = oct_run<kBlock, FAST, true, false>(d, o, dir, inv, 0.01f, tf, st, R, limit, t, hp, c);
+    if (s == RAY_HIT) n = oct_normal_at(d, hp, c);
+    return s;
   }
 };
 
@@ -1154,12 +1165,12 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
       default: launch_render_t<GridS<kGridBuf>, 1>({gd}, s->plane, fa, general, stream, counters, diag); break;
     }
   } else if (s->kind == RT_SCENE_OCTREE) {
-    OctS sc{OctDev{s->d_child, s->d_ovals}};
+    const OctDev od{s->d_child, s->d_ovals};
     switch (s->maxd) {
-      case 4: launch_render_t<OctS, 4>(sc, s->plane, fa, general, stream, counters, diag); break;
-      case 7: launch_render_t<OctS, 7>(sc, s->plane, fa, general, stream, counters, diag); break;
-      case 15: launch_render_t<OctS, 15>(sc, s->plane, fa, general, stream, counters, diag); break;
-      default: launch_render_t<OctS, 31>(sc, s->plane, fa, general, stream, counters, diag); break;
+      case 4: launch_render_t<OctS<true>, 4>(OctS<true>{od}, s->plane, fa, general, stream, counters, diag); break;
+      case 7: launch_render_t<OctS<true>, 7>(OctS<true>{od}, s->plane, fa, general, stream, counters, diag); break;
+      case 15: launch_render_t<OctS<false>, 15>(OctS<false>{od}, s->plane, fa, general, stream, counters, diag); break;
+      default: launch_render_t<OctS<false>, 31>(OctS<false>{od}, s->plane, fa, general, stream, counters, diag); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
@@ -1216,16 +1227,29 @@ bool persist_enabled() {
   return on;
 }
 
-// row-band launches of up to this many ranks take the work queue too
-// (RTAMD_BAND_PERSIST=<N>, A/B switch). Bunny 1080p, max over ranks, 8 frames
-// x 2 streams (ms/frame, queue vs blocks): N = 2 0.0595 vs 0.0607, N = 4
-// 0.0425 vs 0.0342, N = 8 0.0379 vs 0.0218.
-int band_persist_max() {
-  static const int v = [] {
+// Which row-band launches take the work queue. A rank's share of a frame is
+// 1/N of the pixels; below about a million pixels per frame the queue's drain
+// (a wave probes all 8 heads before it exits) and its launch-to-launch
+// hand-over cost more than its balancing gains. Bunny 1080p, max over ranks, 8
+// frames x 2 streams (ms/frame, queue vs blocks): N = 2 (1.04 M px) 0.0595 vs
+// 0.0607, N = 4 0.0425 vs 0.0342, N = 8 0.0379 vs 0.0218. The 1.1 M-triangle
+// stand-in at 4K (2.07 M px per rank at N = 4) took 3.18x at N = 4 on the block
+// dispatch against 1.93x at N = 2 on the queue (profiles/r03/split_mesh_large.txt).
+// RTAMD_BAND_PERSIST=<N> (ranks) or RTAMD_BAND_PERSIST_PX=<pixels> override the
+// rule (A/B switches).
+// (rtx_set_band_queue_px sets the pixel threshold at run time, for tests)
+std::atomic<int64_t> g_band_queue_px{[] {
+  const char *e = std::getenv("RTAMD_BAND_PERSIST_PX");
+  return e ? (int64_t)std::atoll(e) : (int64_t)1000000;
+}()};
+bool band_takes_queue(const FrameArgs &f) {
+  if (f.nranks <= 1) return true;
+  static const int max_ranks = [] {
     const char *e = std::getenv("RTAMD_BAND_PERSIST");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : -1;
   }();
-  return v;
+  if (max_ranks >= 0) return f.nranks <= max_ranks;
+  return (int64_t)f.rows_local * f.W >= g_band_queue_px.load(std::memory_order_relaxed);
 }
 
 // wave tiles per queue item (0: block dispatch); RTAMD_PERSIST_G=1|2|4 overrides
@@ -1316,11 +1340,11 @@ template <class S>
 struct PumpOf {
   static constexpr bool kHas = false;
 };
-template <>
-struct PumpOf<OctS> {
+template <bool PK>
+struct PumpOf<OctS<PK>> {
   static constexpr bool kHas = true;
   using P = OctP;
-  static P make(const OctS &s) { return P{s.d}; }
+  static P make(const OctS<PK> &s) { return P{s.d}; }
 };
 
 template <class P, int MAXD>
@@ -1337,12 +1361,10 @@ int launch_pump_t(const P &sc, const FrameBatch &fb, int n, int group, hipStream
 template <class S, int MAXD>
 int launch_batch_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, bool general,
                    hipStream_t stream) {
-  // Row-band tiles (a rank's share of a multi-GPU frame) of more than 2 ranks
-  // take the block dispatch: with 1/N of the pixels per launch the queue's
-  // drain (a wave probes all 8 heads before it exits) and its launch-to-launch
-  // hand-over cost more than they balance (band_persist_max).
+  // Row-band tiles (a rank's share of a multi-GPU frame) with fewer than about
+  // a million pixels take the block dispatch (band_takes_queue).
   const int group = persist_group(S::kQueueGroup);
-  if (persist_enabled() && group > 0 && fb.f[0].nranks <= band_persist_max()) {
+  if (persist_enabled() && group > 0 && band_takes_queue(fb.f[0])) {
     if constexpr (PumpOf<S>::kHas) {
       if (!general && (pump_env() || (s && s->pump_on)))
         return launch_pump_t<typename PumpOf<S>::P, MAXD>(PumpOf<S>::make(sc), fb, n, group, stream);
@@ -1386,12 +1408,12 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
       default: rc = launch_batch_t<GridS<kGridBuf>, 1>(s, {gd}, s->plane, fb, n, general, stream); break;
     }
   } else if (s->kind == RT_SCENE_OCTREE) {
-    OctS sc{OctDev{s->d_child, s->d_ovals}};
+    const OctDev od{s->d_child, s->d_ovals};
     switch (s->maxd) {
-      case 4: rc = launch_batch_t<OctS, 4>(s, sc, s->plane, fb, n, general, stream); break;
-      case 7: rc = launch_batch_t<OctS, 7>(s, sc, s->plane, fb, n, general, stream); break;
-      case 15: rc = launch_batch_t<OctS, 15>(s, sc, s->plane, fb, n, general, stream); break;
-      default: rc = launch_batch_t<OctS, 31>(s, sc, s->plane, fb, n, general, stream); break;
+      case 4: rc = launch_batch_t<OctS<true>, 4>(s, OctS<true>{od}, s->plane, fb, n, general, stream); break;
+      case 7: rc = launch_batch_t<OctS<true>, 7>(s, OctS<true>{od}, s->plane, fb, n, general, stream); break;
+      case 15: rc = launch_batch_t<OctS<false>, 15>(s, OctS<false>{od}, s->plane, fb, n, general, stream); break;
+      default: rc = launch_batch_t<OctS<false>, 31>(s, OctS<false>{od}, s->plane, fb, n, general, stream); break;
     }
   } else {
     return set_err(RT_E_STATE, "scene has no geometry");
@@ -1961,12 +1983,12 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
         default: launch_rays_t<GridS<kGridBuf>, 1>({gd}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     } else {
-      OctS sc{OctDev{s->d_child, s->d_ovals}};
+      const OctDev od{s->d_child, s->d_ovals};
       switch (s->maxd) {
-        case 4: launch_rays_t<OctS, 4>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        case 7: launch_rays_t<OctS, 7>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        case 15: launch_rays_t<OctS, 15>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
-        default: launch_rays_t<OctS, 31>(sc, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 4: launch_rays_t<OctS<true>, 4>(OctS<true>{od}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 7: launch_rays_t<OctS<true>, 7>(OctS<true>{od}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        case 15: launch_rays_t<OctS<false>, 15>(OctS<false>{od}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
+        default: launch_rays_t<OctS<false>, 31>(OctS<false>{od}, s->plane, dO, dD, n, tnear, tfar, dH, dT, dN, dP); break;
       }
     }
     if ((e = hipGetLastError())) break;
@@ -2134,6 +2156,13 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // Diagnostic: persistent launches from now on write per-wave stamps (see
 // PersistQ::stamps) into the device buffer d_buf of cap_waves x 8 u64
 // (d_buf = NULL turns it off). Not part of include/rtamd.h.
+// Row bands with at least this many pixels per frame take the work queue
+// (band_takes_queue); < 0 restores the default threshold.
+int rtx_set_band_queue_px(int64_t px) {
+  g_band_queue_px.store(px < 0 ? (int64_t)1000000 : px);
+  return RT_OK;
+}
+
 // Builder of this thread's last BVH: 1 host, 2 device, 3 host after a failed
 // device build (AUTO mode falls back; see rtx_bvh_inject_failure)
 int rtx_bvh_last_builder(void) { return t_bvh_last; }

@@ -1067,11 +1067,15 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, float inv
   return normalize(f3{dfdx, dfdy, dfdz});
 }
 
-// intersectLeaf (octree_raytracing.cpp:122-164) for a leaf that may hit.
-template <bool NEED_NORMAL, class CT>
+// intersectLeaf (octree_raytracing.cpp:122-164) for a leaf that may hit. The
+// normal (nodeNormal, :60-118) is NOT evaluated here: a hit returns the march
+// point, and oct_normal_at evaluates it after the traversal loop, where the
+// stack state is dead -- the same arithmetic on the same values, outside the
+// loop's register peak.
+template <class CT>
 __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax,
                                          float inv_s, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                         float &out_t, f3 &out_n, CT &cnt) {
+                                         float &out_t, f3 &out_p, CT &cnt) {
   float t1, t2;
   bbox_intersection(bmin, bmax, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
@@ -1090,13 +1094,37 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
     cnt.add(C_OCT_STEP, 1);
     if (s < 1e-4f) {
       out_t = t + s;
-      if (NEED_NORMAL) { out_n = oct_normal(c, bmin, inv_s, p); cnt.add(C_OCT_NORMAL, 1); }
+      out_p = p;
       return true;
     }
     t += s;
     p = o + t * d;
   }
   return false;
+}
+
+// Where a leaf march hit: the leaf (node index, integer box coordinates at
+// its depth) and the march point, for nodeNormal after the traversal.
+struct OctHitPt {
+  f3 p;
+  uint32_t node, ix, iy, iz;
+  int32_t depth;
+};
+// nodeNormal at a hit (octree_raytracing.cpp:60-118): the leaf's corner
+// values reloaded, its box rebuilt from the coordinates (exact dyadics, the
+// same bits as during the march).
+template <class CT>
+__device__ __forceinline__ f3 oct_normal_at(const OctDev &sc, const OctHitPt &h, CT &cnt) {
+  f3 bmin, bmax;
+  float inv_s;
+  oct_box(h.ix, h.iy, h.iz, h.depth, bmin, bmax, inv_s);
+  OctCorners c;
+  const float4 *q = reinterpret_cast<const float4 *>(sc.vals + h.node);
+  const float4 a = q[0], b = q[1];
+  c.v[0] = a.x; c.v[1] = a.y; c.v[2] = a.z; c.v[3] = a.w;
+  c.v[4] = b.x; c.v[5] = b.y; c.v[6] = b.z; c.v[7] = b.w;
+  cnt.add(C_OCT_NORMAL, 1);
+  return oct_normal(c, bmin, inv_s, h.p);
 }
 
 // the entries of a sorted child list (oct_expand) whose bit is set in keep
@@ -1241,6 +1269,40 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
 // it, whose recursion returns false for every ray, so the first child that
 // hits is the same -- and a child flagged as a leaf that can hit is marched
 // straight away, without loading its word.
+// Integer box coordinates of the top frame's node in the traversal loop.
+// PACK (trees of depth <= 10, which is every tree of up to 7 stack slots): x,
+// y, z in 10-bit fields of one register -- a child is the parent shifted left
+// by one with the child-id bits or'ed in, a pop shifts right and masks -- so
+// the loop carries one register instead of three. Otherwise three words.
+template <bool PACK>
+struct OctXYZ {
+  uint32_t x, y, z;
+  __device__ __forceinline__ OctXYZ(uint32_t ix, uint32_t iy, uint32_t iz) : x(ix), y(iy), z(iz) {}
+  __device__ __forceinline__ OctXYZ child(uint32_t j) const {
+    return OctXYZ((x << 1) | (j >> 2), (y << 1) | ((j >> 1) & 1u), (z << 1) | (j & 1u));
+  }
+  __device__ __forceinline__ void up(uint32_t sh) { x >>= sh; y >>= sh; z >>= sh; }
+  __device__ __forceinline__ uint32_t ix() const { return x; }
+  __device__ __forceinline__ uint32_t iy() const { return y; }
+  __device__ __forceinline__ uint32_t iz() const { return z; }
+};
+template <>
+struct OctXYZ<true> {
+  uint32_t w;  // x | y << 10 | z << 20
+  __device__ __forceinline__ OctXYZ(uint32_t ix, uint32_t iy, uint32_t iz) : w(ix | (iy << 10) | (iz << 20)) {}
+  __device__ __forceinline__ explicit OctXYZ(uint32_t packed, int) : w(packed) {}
+  __device__ __forceinline__ OctXYZ child(uint32_t j) const {
+    return OctXYZ((w << 1) | (j >> 2) | (((j >> 1) & 1u) << 10) | ((j & 1u) << 20), 0);
+  }
+  __device__ __forceinline__ void up(uint32_t sh) {
+    const uint32_t m = 0x3FFu >> sh;
+    w = (w >> sh) & (m | (m << 10) | (m << 20));
+  }
+  __device__ __forceinline__ uint32_t ix() const { return w & 0x3FFu; }
+  __device__ __forceinline__ uint32_t iy() const { return (w >> 10) & 0x3FFu; }
+  __device__ __forceinline__ uint32_t iz() const { return w >> 20; }
+};
+
 struct OctRay {
   uint32_t fbase;
   uint32_t lc;  // remaining child ids (3 bits each, next in the low bits) | count << 24
@@ -1253,18 +1315,18 @@ struct OctRay {
 enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 
 // SDFOctree::intersect -> intersectNode(0) (octree_raytracing.cpp:166-208), root stage.
-template <bool NEED_NORMAL, bool FAST, class CT>
+template <bool FAST, class CT>
 __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                         OctRay &R, float &out_t, f3 &out_n, uint32_t &out_node, CT &cnt) {
+                                         OctRay &R, float &out_t, OctHitPt &hp, CT &cnt) {
   const rtl::OctWord rw = sc.node[0];
   const uint32_t root = rw.child;
   cnt.add(C_OCT_NODE, 1);
   if (root == 0 || root == rtl::kOctNeverHits) {
     cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return RAY_MISS;
-    out_node = 0;
-    return oct_leaf<NEED_NORMAL>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv,
-                                 tNear, tFar, out_t, out_n, cnt)
+    hp.node = 0; hp.ix = 0; hp.iy = 0; hp.iz = 0; hp.depth = 0;
+    return oct_leaf(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar, out_t,
+                    hp.p, cnt)
                ? RAY_HIT
                : RAY_MISS;
   }
@@ -1280,17 +1342,17 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
 // The front-to-back loop of intersectNode below the root. SUSPEND: before each
 // iteration, if `limit` or fewer lanes of the wave are still in the loop, save
 // the state and return RAY_PENDING.
-template <int BLOCK, bool NEED_NORMAL, bool FAST, bool SUSPEND, class CT>
+template <int BLOCK, bool FAST, bool SUSPEND, bool PACK, class CT>
 __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                        LdsStack<BLOCK, kOctFields> st, OctRay &R, int limit, float &out_t,
-                                       f3 &out_n, uint32_t &out_node, CT &cnt) {
+                                       OctHitPt &hp, CT &cnt) {
   constexpr bool MASKS = !CT::kCounts;
   uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24, leafm = R.leafm;
-  uint32_t ix = R.ix, iy = R.iy, iz = R.iz;
+  OctXYZ<PACK> xyz(R.ix, R.iy, R.iz);
   int depth = R.depth, sp = R.sp;
   for (;;) {
     if (SUSPEND && __popcll(__ballot(1)) <= limit) {
-      R = OctRay{fbase, flist | (fcnt << 24), leafm, ix, iy, iz, depth, sp};
+      R = OctRay{fbase, flist | (fcnt << 24), leafm, xyz.ix(), xyz.iy(), xyz.iz(), depth, sp};
       return RAY_PENDING;
     }
     if (fcnt == 0) {
@@ -1301,8 +1363,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
       const uint32_t w2 = st.at(sp, 2);  // leaf mask | depth << 8
       if (MASKS) leafm = w2 & 0xFFu;
       const int d2 = (int)(w2 >> 8);
-      const uint32_t sh = (uint32_t)(depth - d2);
-      ix >>= sh; iy >>= sh; iz >>= sh;
+      xyz.up((uint32_t)(depth - d2));
       depth = d2;
       flist = lc & 0xFFFFFFu;
       fcnt = lc >> 24;  // >= 1: empty frames are never pushed
@@ -1311,7 +1372,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     flist >>= 3;
     fcnt -= 1;
     const uint32_t cn = fbase + j;
-    const uint32_t cx = (ix << 1) | (j >> 2), cy = (iy << 1) | ((j >> 1) & 1u), cz = (iz << 1) | (j & 1u);
+    const OctXYZ<PACK> cxyz = xyz.child(j);
     rtl::OctWord cw{0u, 0u};
     bool leaf;
     if (MASKS) {
@@ -1325,12 +1386,11 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     }
     f3 bmin, bmax;
     float inv_s;
-    oct_box(cx, cy, cz, depth + 1, bmin, bmax, inv_s);
+    oct_box(cxyz.ix(), cxyz.iy(), cxyz.iz(), depth + 1, bmin, bmax, inv_s);
     if (leaf) {
       cnt.add(C_OCT_LEAF, 1);
-      if (oct_leaf<NEED_NORMAL>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, out_n,
-                                cnt)) {
-        out_node = cn;
+      if (oct_leaf(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, hp.p, cnt)) {
+        hp.node = cn; hp.ix = cxyz.ix(); hp.iy = cxyz.iy(); hp.iz = cxyz.iz(); hp.depth = depth + 1;
         return RAY_HIT;
       }
       continue;
@@ -1347,37 +1407,40 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     ++depth;
     fbase = cw.child; flist = l; fcnt = c;
     leafm = cw.masks >> 8;
-    ix = cx; iy = cy; iz = cz;
+    xyz = cxyz;
   }
 }
 
-template <int BLOCK, bool NEED_NORMAL, bool FAST, class CT>
+template <int BLOCK, bool NEED_NORMAL, bool FAST, bool PACK, class CT>
 __device__ __forceinline__ bool oct_trace_t(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear,
                                             float tFar, LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                             uint32_t &out_node, CT &cnt) {
   OctRay R;
-  const int s = oct_start<NEED_NORMAL, FAST>(sc, o, d, inv, tNear, tFar, R, out_t, out_n, out_node, cnt);
-  if (s != RAY_PENDING) return s == RAY_HIT;
-  return oct_run<BLOCK, NEED_NORMAL, FAST, false>(sc, o, d, inv, tNear, tFar, st, R, 0, out_t, out_n, out_node,
-                                                  cnt) == RAY_HIT;
+  OctHitPt hp;
+  int s = oct_start<FAST>(sc, o, d, inv, tNear, tFar, R, out_t, hp, cnt);
+  if (s == RAY_PENDING) s = oct_run<BLOCK, FAST, false, PACK>(sc, o, d, inv, tNear, tFar, st, R, 0, out_t, hp, cnt);
+  if (s != RAY_HIT) return false;
+  out_node = hp.node;
+  if (NEED_NORMAL) out_n = oct_normal_at(sc, hp, cnt);
+  return true;
 }
 
-template <int BLOCK, bool NEED_NORMAL, class CT>
+template <int BLOCK, bool NEED_NORMAL, bool PACK, class CT>
 __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
                                           LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                           uint32_t &out_node, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z))
-    return oct_trace_t<BLOCK, NEED_NORMAL, true>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
-  return oct_trace_t<BLOCK, NEED_NORMAL, false>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
+    return oct_trace_t<BLOCK, NEED_NORMAL, true, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
+  return oct_trace_t<BLOCK, NEED_NORMAL, false, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
 }
 
-template <int BLOCK, class CT>
+template <int BLOCK, bool PACK, class CT>
 __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
                                              LdsStack<BLOCK, kOctFields> st, CT &cnt) {
   Hit h = miss_hit();
   uint32_t node;
-  if (oct_trace<BLOCK, true>(sc, o, d, tNear, tFar, st, h.t, h.n, node, cnt)) {
+  if (oct_trace<BLOCK, true, PACK>(sc, o, d, tNear, tFar, st, h.t, h.n, node, cnt)) {
     h.hit = true;
     h.prim = (int64_t)node;
   } else {
@@ -1385,13 +1448,13 @@ __device__ __forceinline__ Hit oct_intersect(const OctDev &sc, f3 o, f3 d, float
   }
   return h;
 }
-template <int BLOCK, class CT>
+template <int BLOCK, bool PACK, class CT>
 __device__ __forceinline__ bool oct_occluded(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
                                              LdsStack<BLOCK, kOctFields> st, CT &cnt) {
   float t;
   f3 n;
   uint32_t node;
-  return oct_trace<BLOCK, false>(sc, o, d, tNear, tFar, st, t, n, node, cnt);
+  return oct_trace<BLOCK, false, PACK>(sc, o, d, tNear, tFar, st, t, n, node, cnt);
 }
 
 // ------------------------------------------------------------------ plane --
