@@ -34,15 +34,18 @@ for step in "$@"; do
     tests) run tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not fullsize" || exit 1 ;;
     fulltests) run fulltests 600 python -u -m pytest tests/test_fullsize.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
-    bench) run bench 900 python bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/bench_detail.json" && tail -1 "$OUT/bench.log" > "$OUT/bench.json" || exit 1 ;;
-    bench128) run bench128 600 python bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline --no-extra && tail -1 "$OUT/bench128.log" > "$OUT/bench128.json" || exit 1 ;;
+    bench) run bench 900 python bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/bench_detail.json" && grep "^{" "$OUT/bench.log" | tail -n 1 > "$OUT/bench.json" || exit 1 ;;
+    bench128) run bench128 600 python bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline --no-extra && grep "^{" "$OUT/bench128.log" | tail -n 1 > "$OUT/bench128.json" || exit 1 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o p -- python3 bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline || exit 1 ;;
+    prof_driver) run prof_driver 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_driver" -o p -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc --no-cpu-baseline --detail "$OUT/prof_driver_detail.json" || exit 1
+                 grep "^{" "$OUT/prof_driver.log" | tail -n 1 > "$OUT/prof_driver.json"
+                 python tools/prof_summary.py $(ls "$OUT"/prof_driver/*/p_kernel_trace.csv "$OUT"/prof_driver/p_kernel_trace.csv 2>/dev/null | head -n 1) 3 "render_persist_kernel<(anonymous namespace)::MeshS, 4, false>" 2 1 20 > "$OUT/prof_driver_phases.txt" 2>&1; cat "$OUT/prof_driver_phases.txt" ;;
     split) run split 600 python tools/ab.py split bunny || exit 1 ;;
     split_large) run split_large 600 python tools/ab.py split mesh_large || exit 1 ;;
     benchw=*) run "bench_$arg" 600 python bench.py --workload "$arg" --steps 20 --warmup 5 --no-extra \
-                --no-cpu-baseline --detail "$OUT/bench_${arg}_detail.json" && tail -1 "$OUT/bench_$arg.log" > "$OUT/bench_$arg.json" || exit 1 ;;
-    dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && tail -1 "$OUT/dist_gloo.log" > "$OUT/dist_gloo.json" || exit 1 ;;
-    dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && tail -1 "$OUT/dist_rccl1.log" > "$OUT/dist_rccl1.json" || exit 1 ;;
+                --no-cpu-baseline --detail "$OUT/bench_${arg}_detail.json" && grep "^{" "$OUT/bench_$arg.log" | tail -n 1 > "$OUT/bench_$arg.json" || exit 1 ;;
+    dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && grep "^{" "$OUT/dist_gloo.log" | tail -n 1 > "$OUT/dist_gloo.json" || exit 1 ;;
+    dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && grep "^{" "$OUT/dist_rccl1.log" | tail -n 1 > "$OUT/dist_rccl1.json" || exit 1 ;;
     ab=*) echo "== $tag [$arg]"; run "$tag" 300 env "${envs[@]}" python tools/ab.py batch ${AB_WL:-bunny} || exit 1
           grep -v amdgpu "$OUT/$tag.log" ;;
     ptest=*) run "$tag" 600 env "${envs[@]}" python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "${AB_K:-not fullsize}" || exit 1 ;;

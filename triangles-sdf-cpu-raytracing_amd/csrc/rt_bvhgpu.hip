@@ -15,15 +15,17 @@
 //    and the final insertion sort in one thread each;
 //  * the final insertion sort never moves an element across a partition
 //    boundary, so sorting each leaf segment separately gives the same order.
-// The SAH sweeps (triangles_raytracing.cpp:53-98) are one workgroup per
-// (candidate, axis): a reverse scan for the right boxes, a forward scan for
-// the left boxes and the cost, and the first minimum. The breadth-first
+// The SAH sweeps (triangles_raytracing.cpp:53-98) cut every (candidate, axis)
+// range into chunks of 2048 triangles, one workgroup each: chunk unions, their
+// prefix / suffix per range, then each chunk's right boxes (reverse scan),
+// left boxes (forward scan), costs and first minimum. The breadth-first
 // candidate queue of createNode (:155-225, at most 7 splits) is driven from
 // the host, one candidate layer of every open node per stage; candidates the
 // reference never reaches once a node has 7 splits are evaluated
 // speculatively and rolled back (their range restored), because tryDivide
 // re-sorts its range even when it does not split.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -41,7 +43,10 @@
 
 namespace {
 
-constexpr uint32_t kSerialMax = 256;  // segments at most this long: one wave, serial introsort in LDS
+#ifndef RT_SERIAL_MAX
+#define RT_SERIAL_MAX 256  // A/B switch
+#endif
+constexpr uint32_t kSerialMax = RT_SERIAL_MAX;  // segments at most this long: one wave, serial introsort in LDS
 constexpr int kScanT = 256, kScanI = 8, kScanBlk = kScanT * kScanI;
 
 struct Seg {
@@ -205,7 +210,16 @@ __global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t *ids, c
 }
 
 // ---- inclusive scan of u32 (three launches) --------------------------------
-__global__ __launch_bounds__(kScanT) void k_scan1(const uint32_t *in, uint32_t *out, uint32_t *bsum, uint32_t n) {
+// blockIdx.y (k_scan1, k_scan3) / blockIdx.x (k_scan2) selects one of two
+// independent arrays, so the partition round's two flag scans share launches
+struct ScanPair {
+  const uint32_t *in[2];
+  uint32_t *out[2];
+  uint32_t *bsum[2];
+};
+__global__ __launch_bounds__(kScanT) void k_scan1(ScanPair sp, uint32_t n) {
+  const uint32_t *in = sp.in[blockIdx.y];
+  uint32_t *out = sp.out[blockIdx.y], *bsum = sp.bsum[blockIdx.y];
   __shared__ uint32_t sm[kScanT];
   const uint32_t base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
   uint32_t v[kScanI], acc = 0;
@@ -228,7 +242,8 @@ __global__ __launch_bounds__(kScanT) void k_scan1(const uint32_t *in, uint32_t *
     if (base + k < n) out[base + k] = v[k] + ex;
   if (threadIdx.x == kScanT - 1) bsum[blockIdx.x] = sm[kScanT - 1];
 }
-__global__ __launch_bounds__(1024) void k_scan2(uint32_t *bsum, uint32_t nb) {
+__global__ __launch_bounds__(1024) void k_scan2(ScanPair sp, uint32_t nb) {
+  uint32_t *bsum = sp.bsum[blockIdx.x];
   __shared__ uint32_t sm[1024];
   const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
   uint32_t acc = 0;
@@ -249,7 +264,9 @@ __global__ __launch_bounds__(1024) void k_scan2(uint32_t *bsum, uint32_t nb) {
       bsum[b0 + k] = run;
     }
 }
-__global__ __launch_bounds__(kScanT) void k_scan3(uint32_t *out, const uint32_t *bsum, uint32_t n) {
+__global__ __launch_bounds__(kScanT) void k_scan3(ScanPair sp, uint32_t n) {
+  uint32_t *out = sp.out[blockIdx.y];
+  const uint32_t *bsum = sp.bsum[blockIdx.y];
   if (blockIdx.x == 0) return;
   const uint32_t add = bsum[blockIdx.x - 1], base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
 #pragma unroll
@@ -432,71 +449,122 @@ struct Task {
   uint32_t s, e;  // triangle range [s, e) of one candidate
 };
 
-// The sweeps of tryDivide(indices, start, end, axis) on the sorted range:
-// each thread takes kSahI consecutive triangles of a chunk, accumulated in the
-// order the reference accumulates them (the right boxes from the end, the
-// left boxes from the start), then a block scan over the threads and the
-// carry of the previous chunks; every union keeps the earlier operand.
-__global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t *ids3, const TBox *tbox, uint32_t n,
-                                               TBox *rightB3, float *out_cost, uint32_t *out_div) {
+// ---- SAH sweeps over chunks: many workgroups per (candidate, axis) ----------
+// The sweep above walks a whole candidate range in ONE workgroup, so the top
+// stages (a handful of candidates over up to 3n triangles) ran on 3-6
+// workgroups. Here a (candidate, axis) range is cut into chunks of kSahChunk
+// triangles: (1) every chunk's box union, (2) per (candidate, axis) the
+// exclusive prefix and suffix unions of its chunks (one thread walks them),
+// (3) every chunk's dividers -- right boxes by a reverse scan inside the chunk
+// plus the suffix of the chunks after it, left boxes by a forward scan plus
+// the prefix -- and the chunk's first minimum; the host takes the first
+// minimum over the chunks. Box unions are exact min / max, so the areas, and
+// with them every cost, are the sequential sweep's values.
+struct SahChunk {
+  uint32_t task, axis, lo, hi;  // triangle range [lo, hi) of candidate `task` on `axis`
+  uint32_t group;               // task * 3 + axis
+};
+struct SahGroup {
+  uint32_t first, count;  // its chunks
+};
+
+__global__ __launch_bounds__(kSahT) void k_sah_chunk_box(const SahChunk *chunks, const uint32_t *ids3,
+                                                         const TBox *tbox, uint32_t n, TBox *cbox) {
   __shared__ TBox sm[kSahT];
-  __shared__ float s_psa;
+  const SahChunk c = chunks[blockIdx.x];
+  const uint32_t *ids = ids3 + c.axis * n;
+  TBox acc = tb_empty();
+  const uint32_t t0 = c.lo + threadIdx.x * kSahI;
+#pragma unroll
+  for (int q = 0; q < kSahI; ++q)
+    if (t0 + q < c.hi) acc = tb_union(acc, tbox[ids[t0 + q]]);
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t o = 1; o < (uint32_t)kSahT; o <<= 1) {
+    if ((threadIdx.x & (2 * o - 1)) == 0) sm[threadIdx.x] = tb_union(sm[threadIdx.x], sm[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cbox[blockIdx.x] = sm[0];
+}
+
+// one thread per (candidate, axis): exclusive prefix / suffix unions of its
+// chunks, and the parent's surface area (:84, the union of the whole range)
+__global__ void k_sah_carry(const SahGroup *groups, uint32_t ng, const TBox *cbox, TBox *cpre, TBox *csuf,
+                            float *psa) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const SahGroup G = groups[g];
+  TBox a = tb_empty();
+  for (uint32_t k = 0; k < G.count; ++k) {
+    cpre[G.first + k] = a;
+    a = tb_union(a, cbox[G.first + k]);
+  }
+  psa[g] = tb_area(a);
+  TBox b = tb_empty();
+  for (uint32_t k = G.count; k-- > 0;) {
+    csuf[G.first + k] = b;
+    b = tb_union(cbox[G.first + k], b);
+  }
+}
+
+__global__ __launch_bounds__(kSahT) void k_sah_chunk_cost(const SahChunk *chunks, const Task *tasks,
+                                                          const uint32_t *ids3, const TBox *tbox, uint32_t n,
+                                                          const TBox *cpre, const TBox *csuf, const float *psa_g,
+                                                          float *ccost, uint32_t *cdiv) {
+  __shared__ TBox sm[kSahT];
   __shared__ float s_cost[kSahT];
   __shared__ uint32_t s_div[kSahT];
-  const Task tk = tasks[blockIdx.x / 3];
-  const uint32_t base = (blockIdx.x % 3) * n;
-  const uint32_t *ids = ids3 + base;
-  TBox *rightB = rightB3 + base;
-  // right boxes: union over [t, e), built from the end (triangles_raytracing.cpp:67-80)
-  TBox carry = tb_empty();
-  for (int64_t hi = tk.e; hi > (int64_t)tk.s; hi -= kSahChunk) {
-    TBox loc = tb_empty(), tot;
-    const int64_t t0 = hi - 1 - (int64_t)threadIdx.x * kSahI;  // this thread: t0, t0 - 1, ...
+  const SahChunk c = chunks[blockIdx.x];
+  const Task tk = tasks[c.task];
+  const uint32_t *ids = ids3 + c.axis * n;
+  const float psa = psa_g[c.group];
+  const uint32_t t0 = c.lo + threadIdx.x * kSahI;
+  TBox tb[kSahI];
+  TBox loc = tb_empty();
 #pragma unroll
-    for (int q = 0; q < kSahI; ++q)
-      if (t0 - q >= (int64_t)tk.s) loc = tb_union(loc, tbox[ids[t0 - q]]);
-    const TBox pre = tb_union(carry, block_excl_box(loc, sm, &tot));
-    TBox r = pre;
+  for (int q = 0; q < kSahI; ++q) {
+    tb[q] = (t0 + q < c.hi) ? tbox[ids[t0 + q]] : tb_empty();
+    loc = tb_union(loc, tb[q]);
+  }
+  // right boxes: the union of everything after triangle t, t = t0 + q
+  // (threads after this one in the chunk: a reverse exclusive scan; chunks
+  // after this one: csuf)
+  sm[threadIdx.x] = loc;
+  __syncthreads();
+  for (int o = 1; o < kSahT; o <<= 1) {
+    TBox x = tb_empty();
+    if (threadIdx.x + (uint32_t)o < (uint32_t)kSahT) x = sm[threadIdx.x + o];
+    __syncthreads();
+    sm[threadIdx.x] = tb_union(sm[threadIdx.x], x);
+    __syncthreads();
+  }
+  TBox r = tb_union(threadIdx.x + 1 < (uint32_t)kSahT ? sm[threadIdx.x + 1] : tb_empty(), csuf[blockIdx.x]);
+  float rarea[kSahI];
 #pragma unroll
-    for (int q = 0; q < kSahI; ++q) {
-      const int64_t t = t0 - q;
-      if (t >= (int64_t)tk.s) {
-        r = tb_union(r, tbox[ids[t]]);
-        rightB[t] = r;
-      }
-    }
-    carry = tb_union(carry, tot);
+  for (int q = kSahI - 1; q >= 0; --q) {
+    rarea[q] = tb_area(r);
+    r = tb_union(tb[q], r);
   }
   __syncthreads();
-  if (threadIdx.x == 0) s_psa = tb_area(rightB[tk.s]);  // parent box (:84)
-  __syncthreads();
-  const float psa = s_psa;
-  // left boxes and the cost of every divider (:85-98); first minimum
+  // left boxes: everything up to and including triangle t (chunks before:
+  // cpre; threads before this one: an exclusive scan)
+  TBox tot;
+  TBox left = tb_union(cpre[blockIdx.x], block_excl_box(loc, sm, &tot));
   float best = __builtin_huge_valf();
   uint32_t bdiv = 0xFFFFFFFFu;
-  carry = tb_empty();
-  for (uint32_t lo = tk.s; lo < tk.e; lo += kSahChunk) {
-    TBox loc = tb_empty(), tot;
-    const uint32_t t0 = lo + threadIdx.x * kSahI;
 #pragma unroll
-    for (int q = 0; q < kSahI; ++q)
-      if (t0 + q < tk.e) loc = tb_union(loc, tbox[ids[t0 + q]]);
-    TBox left = tb_union(carry, block_excl_box(loc, sm, &tot));
-#pragma unroll
-    for (int q = 0; q < kSahI; ++q) {
-      const uint32_t t = t0 + q, d = t + 1;  // divider after triangle t (index units: 3 d)
-      if (t < tk.e) left = tb_union(left, tbox[ids[t]]);
-      if (d < tk.e) {
-        const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
-        const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
-        const float c = 0.2f + tb_area(left) / psa * lc + tb_area(rightB[d]) / psa * rc;
-        if (c < best) {  // NaN never wins, as `curSAH < result.sah`; a thread's dividers ascend
-          best = c;
-          bdiv = d;
-        }
+  for (int q = 0; q < kSahI; ++q) {
+    const uint32_t t = t0 + q, d = t + 1;  // divider after triangle t (index units: 3 d)
+    if (t < c.hi) left = tb_union(left, tb[q]);
+    if (t < c.hi && d < tk.e) {
+      const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
+      const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
+      const float cost = 0.2f + tb_area(left) / psa * lc + rarea[q] / psa * rc;
+      if (cost < best) {  // NaN never wins, as `curSAH < result.sah`; a thread's dividers ascend
+        best = cost;
+        bdiv = d;
       }
     }
-    carry = tb_union(carry, tot);
   }
   s_cost[threadIdx.x] = best;
   s_div[threadIdx.x] = bdiv;
@@ -513,15 +581,18 @@ __global__ __launch_bounds__(kSahT) void k_sah(const Task *tasks, const uint32_t
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    out_cost[blockIdx.x] = s_cost[0];
-    out_div[blockIdx.x] = s_div[0];
+    ccost[blockIdx.x] = s_cost[0];
+    cdiv[blockIdx.x] = s_div[0];
   }
 }
 
-// stage start: every candidate range saved (rollback) and copied to the Y / Z scratch
-__global__ void k_stage_copy(const Task *tasks, uint32_t *ids3, uint32_t *backup, uint32_t n) {
-  const Task tk = tasks[blockIdx.x];
-  for (uint32_t t = tk.s + threadIdx.x; t < tk.e; t += blockDim.x) {
+// stage start: every candidate range saved (rollback) and copied to the Y / Z
+// scratch; one workgroup per kSahChunk-triangle chunk of a candidate (the axis-0
+// chunks of the SAH table), so a stage of a few huge candidates is not left to
+// a few workgroups
+__global__ void k_stage_copy(const SahChunk *chunks, uint32_t *ids3, uint32_t *backup, uint32_t n) {
+  const SahChunk c = chunks[blockIdx.x];
+  for (uint32_t t = c.lo + threadIdx.x; t < c.hi; t += blockDim.x) {
     const uint32_t v = ids3[t];
     backup[t] = v;
     ids3[n + t] = v;
@@ -529,13 +600,23 @@ __global__ void k_stage_copy(const Task *tasks, uint32_t *ids3, uint32_t *backup
   }
 }
 // stage end: 1 = take the Y order, 2 = the Z order, 3 = restore (never evaluated by the reference)
-__global__ void k_stage_apply(const Task *tasks, const uint32_t *action, uint32_t *ids3, const uint32_t *backup,
+__global__ void k_stage_apply(const SahChunk *chunks, const uint32_t *action, uint32_t *ids3, const uint32_t *backup,
                               uint32_t n) {
-  const Task tk = tasks[blockIdx.x];
-  const uint32_t a = action[blockIdx.x];
+  const SahChunk c = chunks[blockIdx.x];
+  const uint32_t a = action[c.task];
   if (a == 0) return;
   const uint32_t *src = a == 1 ? ids3 + n : a == 2 ? ids3 + 2 * n : backup;
-  for (uint32_t t = tk.s + threadIdx.x; t < tk.e; t += blockDim.x) ids3[t] = src[t];
+  for (uint32_t t = c.lo + threadIdx.x; t < c.hi; t += blockDim.x) ids3[t] = src[t];
+}
+// child boxes (calc_bbox, :199): the ordered fold of a range's chunk unions
+// (k_sah_chunk_box on its chunks), earlier chunk on the left
+__global__ void k_group_fold(const SahGroup *groups, uint32_t ng, const TBox *cbox, TBox *out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const SahGroup G = groups[g];
+  TBox a = tb_empty();
+  for (uint32_t k = 0; k < G.count; ++k) a = tb_union(a, cbox[G.first + k]);
+  out[g] = a;
 }
 
 // per-triangle box (calc_bbox of the /w-divided vertices, raytracing.hpp:51-60) and keys
@@ -555,35 +636,16 @@ __global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TB
   K3[2 * n + t] = b.mx[2];
 }
 
-// child boxes: union over a final triangle range (calc_bbox(m_mesh, lo, hi), :199)
-__global__ __launch_bounds__(kSahT) void k_range_box(const Task *ranges, const uint32_t *ids, const TBox *tbox,
-                                                     TBox *out) {
-  __shared__ TBox sm[kSahT];
-  const Task r = ranges[blockIdx.x];
-  // contiguous chunks, combined in order: among equal bounds (+0 / -0) the
-  // first in range order is kept, as the sequential std::min / std::max do
-  const uint32_t len = r.e - r.s, per = (len + kSahT - 1) / kSahT;
-  const uint32_t t0 = r.s + threadIdx.x * per, t1 = min(r.e, t0 + per);
-  TBox acc = tb_empty();
-  for (uint32_t t = t0; t < t1; ++t) acc = tb_union(acc, tbox[ids[t]]);
-  sm[threadIdx.x] = acc;
-  __syncthreads();
-  // pairwise over ADJACENT chunk ranges, the earlier one on the left, so the
-  // union stays the sequential left fold (a strided tree would pair chunk i
-  // with chunk i + kSahT/2 first and keep a later equal bound)
-  for (uint32_t o = 1; o < (uint32_t)kSahT; o <<= 1) {
-    if ((threadIdx.x & (2 * o - 1)) == 0) sm[threadIdx.x] = tb_union(sm[threadIdx.x], sm[threadIdx.x + o]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
-}
-
 // ---- host side ---------------------------------------------------------------
 // RTAMD_BVH_TIMING=1: per-phase wall time of a device build on stderr (the
 // phases are synchronised for the measurement)
 struct PhaseTimer {
   bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
   double acc[8] = {};
+  double host[4] = {};  // wall time of host-side stage sections (no syncs): prologue, FIFO, apply+boxes
+  std::chrono::steady_clock::time_point h0;
+  void hstart() { h0 = std::chrono::steady_clock::now(); }
+  void hstop(int k) { host[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); }
   int rounds = 0, stages = 0, serial_launches = 0;
   std::chrono::steady_clock::time_point t0;
   hipStream_t st = nullptr;
@@ -606,13 +668,17 @@ struct DBuf {
   ~DBuf() {
     if (p) (void)hipFree(p);
   }
+  // grows geometrically: the per-stage buffers widen with the tree, and a
+  // hipFree / hipMalloc pair at every stage for each of them synchronises the
+  // device each time
   int reserve(size_t n) {
     if (n <= cap) return RT_OK;
+    const size_t want = std::max<size_t>({n, 2 * cap, 1024});
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    HIP_TRY(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
-    cap = n;
+    HIP_TRY(hipMalloc(&p, want * sizeof(T)));
+    cap = want;
     return RT_OK;
   }
 };
@@ -629,6 +695,7 @@ struct Sorter {
   DBuf<Seg> segA, segB, serial;
   DBuf<uint32_t> size, offs, sw, af, bf, Ai, Bi, segv, Lpos, Rpos, bsum, ctr;
   DBuf<float> kp;
+  size_t bsum_half = 0;  // bsum: two halves, one per array of a paired scan
   hipStream_t st = nullptr;
   PhaseTimer own_pt;             // per build: concurrent builds share no state
   PhaseTimer *pt = &own_pt;
@@ -643,18 +710,22 @@ struct Sorter {
         (rc = size.reserve(segcap + 1)) || (rc = offs.reserve(segcap + 1)) || (rc = sw.reserve(segcap)) ||
         (rc = kp.reserve(segcap)) || (rc = af.reserve(N)) || (rc = bf.reserve(N)) || (rc = Ai.reserve(N)) ||
         (rc = Bi.reserve(N)) || (rc = segv.reserve(N)) || (rc = Lpos.reserve(N)) || (rc = Rpos.reserve(N)) ||
-        (rc = bsum.reserve(N / kScanBlk + 2)) || (rc = ctr.reserve(4)))
+        (rc = bsum.reserve(2 * (N / kScanBlk + 2))) || (rc = ctr.reserve(4)))
       return rc;
+    bsum_half = N / kScanBlk + 2;
     return RT_OK;
   }
 
-  int scan(const uint32_t *in, uint32_t *out, uint32_t cnt) {
+  // inclusive scans of one array (in1 == nullptr) or of two at once
+  int scan(const uint32_t *in, uint32_t *out, uint32_t cnt, const uint32_t *in1 = nullptr,
+           uint32_t *out1 = nullptr) {
     if (cnt == 0) return RT_OK;
-    const uint32_t nb = (cnt + kScanBlk - 1) / kScanBlk;
-    k_scan1<<<nb, kScanT, 0, st>>>(in, out, bsum.p, cnt);
+    const uint32_t nb = (cnt + kScanBlk - 1) / kScanBlk, na = in1 ? 2u : 1u;
+    const ScanPair sp{{in, in1}, {out, out1}, {bsum.p, bsum.p + bsum_half}};
+    k_scan1<<<dim3(nb, na), kScanT, 0, st>>>(sp, cnt);
     if (nb > 1) {
-      k_scan2<<<1, 1024, 0, st>>>(bsum.p, nb);
-      k_scan3<<<nb, kScanT, 0, st>>>(out, bsum.p, cnt);
+      k_scan2<<<na, 1024, 0, st>>>(sp, nb);
+      k_scan3<<<dim3(nb, na), kScanT, 0, st>>>(sp, cnt);
     }
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -686,8 +757,7 @@ struct Sorter {
       const uint32_t ge = (E + 255) / 256;
       if (E) {
         k_flags<<<ge, 256, 0, st>>>(cur, offs.p, m, ids, K3, n, kp.p, af.p, bf.p, segv.p, E);
-        if (int rc = scan(af.p, Ai.p, E)) return rc;
-        if (int rc = scan(bf.p, Bi.p, E)) return rc;
+        if (int rc = scan(af.p, Ai.p, E, bf.p, Bi.p)) return rc;
         k_ranks<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, bf.p, Ai.p, Bi.p, segv.p, Lpos.p, Rpos.p, E);
         k_swaps_count<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, Bi.p, segv.p, Lpos.p, sw.p, E);
         k_swap<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, segv.p, Rpos.p, sw.p, ids, E);
@@ -713,11 +783,59 @@ struct Sorter {
   }
 };
 
+// The device build's host-side node array (createNode's m_nodes). Up to 2n - 1
+// nodes of ~240 B are written once each as the build proceeds; backed by an
+// anonymous mapping of that bound with transparent huge pages requested, so a
+// 1.1 M-triangle build's ~40 MB of nodes are ~20 page faults instead of ~10^4
+// (untouched pages of the reservation cost nothing).
+struct NodeArena {
+  rth::BvhHostNode *p = nullptr;
+  size_t n = 0, cap = 0, bytes = 0;
+  NodeArena() = default;
+  NodeArena(const NodeArena &) = delete;
+  NodeArena &operator=(const NodeArena &) = delete;
+  ~NodeArena() {
+    if (p) munmap(p, bytes);
+  }
+  bool reserve(size_t c) {
+    const size_t huge = (size_t)2 << 20;
+    bytes = (c * sizeof(rth::BvhHostNode) + huge - 1) / huge * huge;
+    void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) return false;
+    (void)madvise(m, bytes, MADV_HUGEPAGE);
+    p = static_cast<rth::BvhHostNode *>(m);
+    cap = c;
+    return true;
+  }
+  size_t size() const { return n; }
+  rth::BvhHostNode &operator[](size_t i) { return p[i]; }
+  void emplace_back() { new (p + n++) rth::BvhHostNode(); }  // n < cap: at most 2 ntri - 1 nodes
+};
+
+// createNode's ChipQueue contents (FIFO). A node splits at most 7 times and
+// its queue is dropped at the 7th split, so it never holds more than 8
+// candidates (a layer of 4 that all split reaches 7 splits); kept inline, so
+// the ~10^5 open nodes of a large build allocate nothing
+struct CandQueue {
+  std::pair<uint32_t, uint32_t> a[16];
+  uint32_t n = 0;
+  const std::pair<uint32_t, uint32_t> *begin() const { return a; }
+  const std::pair<uint32_t, uint32_t> *end() const { return a + n; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const std::pair<uint32_t, uint32_t> &operator[](size_t i) const { return a[i]; }
+  void push_back(std::pair<uint32_t, uint32_t> c) { a[n < 16 ? n++ : 15] = c; }
+  static CandQueue of(uint32_t lo, uint32_t hi) {
+    CandQueue q;
+    q.push_back({lo, hi});
+    return q;
+  }
+};
 // BVHBuilder::createNode state of one node (triangles_raytracing.cpp:155-225)
 struct Open {
   int32_t node;
   uint32_t start, end;  // index units
-  std::vector<std::pair<uint32_t, uint32_t>> queue;  // ChipQueue contents, FIFO
+  CandQueue queue;
   uint32_t div[8];
   int nd = 0;
 };
@@ -758,14 +876,23 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
 
   const auto tb0 = std::chrono::steady_clock::now();
   PhaseTimer pt;
+  pt.start();
   DBuf<float4> dv;
   DBuf<uint32_t> didx, ids3, backup, ddiv, dact;
   DBuf<float> K3, dcost;
-  DBuf<TBox> tbox, rightB3, boxes;
+  DBuf<TBox> tbox, boxes, cbox, cpre, csuf;
   DBuf<Task> dtasks;
+  DBuf<SahChunk> dchunks, drch;
+  DBuf<SahGroup> dgroups, drgrp;
+  DBuf<TBox> rcbox;
+  std::vector<SahChunk> ch, rch;  // per-stage chunk tables (host copies)
+  std::vector<SahGroup> grp, rgrp;
+  uint32_t NC = 0, NC0 = 0;
+  DBuf<float> ccost, dpsa;
+  DBuf<uint32_t> cdivv;
   Sorter S;
   if (dv.reserve((size_t)nverts) || didx.reserve((size_t)nidx) || ids3.reserve(3 * (size_t)n) ||
-      backup.reserve(n) || K3.reserve(3 * (size_t)n) || tbox.reserve(n) || rightB3.reserve(3 * (size_t)n) ||
+      backup.reserve(n) || K3.reserve(3 * (size_t)n) || tbox.reserve(n) ||
       S.init(n, nullptr, nullptr))
     return fail("allocation");
   S.ids = ids3.p;
@@ -786,10 +913,21 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   BVH_DEV(hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st), "upload");
   k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p);
   BVH_DEV(hipGetLastError(), "triangle boxes");
+  pt.stop(7);  // allocation, upload, triangle boxes
 
-  std::vector<BvhHostNode> H(1);
-  std::vector<Open> open;
-  open.push_back(Open{0, 0, 3 * n, {{0u, 3 * n}}, {}, 0});
+  // host state reused across the stages (cleared, never freed: fresh pages
+  // of per-stage vectors cost more than the stage logic itself)
+  NodeArena H;
+  if (!H.reserve(2 * (size_t)n + 1)) return hfail("node arena", hipErrorOutOfMemory);
+  H.emplace_back();
+  std::vector<Open> open, next;
+  std::vector<Task> tasks;
+  std::vector<int> task_of;
+  std::vector<uint32_t> task_off, dvd, action;
+  std::vector<float> cost, hcc;
+  std::vector<uint32_t> hcd;
+  std::vector<Seg> segs;
+  open.push_back(Open{0, 0, 3 * n, CandQueue::of(0u, 3 * n), {}, 0});
   // child ranges (triangle units) and their boxes: a node's child boxes are
   // computed in the stage that completes the node, over the triangle order at
   // that point (calc_bbox at creation, triangles_raytracing.cpp:199), before
@@ -799,53 +937,97 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   std::vector<std::pair<int32_t, int>> range_of;  // (node, child slot) per range
   const size_t max_ranges = 2 * (size_t)n + 8;    // every node but the root is a child range
   ranges.reserve(max_ranges);
-  DBuf<Task> dranges;
-  if (dranges.reserve(max_ranges) || boxes.reserve(max_ranges)) return fail("allocation");
-  pt.start();
-  pt.stop(7);  // allocation + upload
+  range_of.reserve(max_ranges);
+  if (boxes.reserve(max_ranges)) return fail("allocation");
+  const auto ts0 = std::chrono::steady_clock::now();
   while (!open.empty()) {
     ++pt.stages;
+    pt.hstart();
     const size_t r0 = ranges.size();
     // this stage: every queued candidate of every open node that tryDivide sorts (> 8 triangles)
-    std::vector<Task> tasks;
-    std::vector<std::vector<int>> task_of(open.size());
-    for (size_t o = 0; o < open.size(); ++o)
+    tasks.clear();
+    // task index of open node o's candidate c: task_of[task_off[o] + c] (-1: not sorted)
+    task_of.clear();
+    task_off.resize(open.size());
+    for (size_t o = 0; o < open.size(); ++o) {
+      task_off[o] = (uint32_t)task_of.size();
       for (auto &c : open[o].queue) {
         const bool gpu = c.second - c.first > 24;
-        task_of[o].push_back(gpu ? (int)tasks.size() : -1);
+        task_of.push_back(gpu ? (int)tasks.size() : -1);
         if (gpu) tasks.push_back(Task{c.first / 3, c.second / 3});
       }
+    }
     const uint32_t T = (uint32_t)tasks.size();
-    std::vector<float> cost(3 * (size_t)T);
-    std::vector<uint32_t> dvd(3 * (size_t)T), action(T, 0);
+    cost.assign(3 * (size_t)T, 0.0f);
+    dvd.assign(3 * (size_t)T, 0u);
+    action.assign(T, 0u);
     if (T) {
       if (dtasks.reserve(T) || dcost.reserve(3 * (size_t)T) || ddiv.reserve(3 * (size_t)T) || dact.reserve(T))
         return fail("allocation");
       BVH_DEV(hipMemcpyAsync(dtasks.p, tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st), "upload");
-      k_stage_copy<<<T, 256, 0, st>>>(dtasks.p, ids3.p, backup.p, n);
-      std::vector<Seg> segs;
+      // chunks of every (candidate, axis) range: [axis-0 chunks of all candidates | axis 1 | axis 2]
+      ch.clear();
+      grp.assign(3 * (size_t)T, SahGroup{});
+      for (uint32_t a = 0; a < 3; ++a)
+        for (uint32_t ti = 0; ti < T; ++ti) {
+          SahGroup &G = grp[3 * ti + a];
+          G.first = (uint32_t)ch.size();
+          for (uint32_t lo = tasks[ti].s; lo < tasks[ti].e; lo += kSahChunk)
+            ch.push_back(SahChunk{ti, a, lo, std::min<uint32_t>(tasks[ti].e, lo + kSahChunk), 3 * ti + a});
+          G.count = (uint32_t)ch.size() - G.first;
+        }
+      NC = (uint32_t)ch.size();
+      NC0 = NC / 3;  // the axis-0 chunks come first
+      const uint32_t NG = 3 * T;
+      if (dchunks.reserve(NC) || dgroups.reserve(NG) || cbox.reserve(NC) || cpre.reserve(NC) || csuf.reserve(NC) ||
+          ccost.reserve(NC) || cdivv.reserve(NC) || dpsa.reserve(NG))
+        return fail("allocation");
+      BVH_DEV(hipMemcpyAsync(dchunks.p, ch.data(), NC * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(dgroups.p, grp.data(), NG * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
+      k_stage_copy<<<NC0, 256, 0, st>>>(dchunks.p, ids3.p, backup.p, n);
+      segs.clear();
       segs.reserve(3 * (size_t)T);
       for (int a = 0; a < 3; ++a)
         for (const Task &tk : tasks)
           segs.push_back(Seg{a * n + tk.s, a * n + tk.e, 2 * lg2(tk.e - tk.s), 0});
+      pt.hstop(0);
       if (S.sort(segs)) return fail("sort");
       pt.start();
-      k_sah<<<3 * T, kSahT, 0, st>>>(dtasks.p, ids3.p, tbox.p, n, rightB3.p, dcost.p, ddiv.p);
-      pt.stop(2);
+      k_sah_chunk_box<<<NC, kSahT, 0, st>>>(dchunks.p, ids3.p, tbox.p, n, cbox.p);
+      k_sah_carry<<<(NG + 63) / 64, 64, 0, st>>>(dgroups.p, NG, cbox.p, cpre.p, csuf.p, dpsa.p);
+      k_sah_chunk_cost<<<NC, kSahT, 0, st>>>(dchunks.p, dtasks.p, ids3.p, tbox.p, n, cpre.p, csuf.p, dpsa.p, ccost.p,
+                                             cdivv.p);
       BVH_DEV(hipGetLastError(), "SAH sweep");
-      BVH_DEV(hipMemcpyAsync(cost.data(), dcost.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
-      BVH_DEV(hipMemcpyAsync(dvd.data(), ddiv.p, 3 * (size_t)T * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
+      hcc.resize(NC);
+      hcd.resize(NC);
+      BVH_DEV(hipMemcpyAsync(hcc.data(), ccost.p, NC * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
+      BVH_DEV(hipMemcpyAsync(hcd.data(), cdivv.p, NC * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
       BVH_DEV(hipStreamSynchronize(st), "SAH sweep");
+      pt.stop(2);
+      // first minimum over the chunks of each (candidate, axis): (cost, divider) lexicographic
+      for (uint32_t g = 0; g < NG; ++g) {
+        float bc = __builtin_huge_valf();
+        uint32_t bd = 0xFFFFFFFFu;
+        for (uint32_t k = grp[g].first; k < grp[g].first + grp[g].count; ++k)
+          if (hcc[k] < bc || (hcc[k] == bc && hcd[k] < bd)) {
+            bc = hcc[k];
+            bd = hcd[k];
+          }
+        // cost/dvd are indexed [3 * task + axis], as the single-workgroup sweep wrote them
+        cost[g] = bc;
+        dvd[g] = bd;
+      }
     }
+    pt.hstart();
     // createNode's FIFO, candidate by candidate (triangles_raytracing.cpp:162-173)
-    std::vector<Open> next;
+    next.clear();
     for (size_t o = 0; o < open.size(); ++o) {
       Open &N = open[o];
-      std::vector<std::pair<uint32_t, uint32_t>> q2;
+      CandQueue q2;
       bool capped = false;
       for (size_t c = 0; c < N.queue.size(); ++c) {
         const auto cand = N.queue[c];
-        const int ti = task_of[o][c];
+        const int ti = task_of[task_off[o] + c];
         if (N.nd == 7) {  // the reference stops here: this candidate is never tried
           capped = true;
           if (ti >= 0) action[ti] = 3;
@@ -883,7 +1065,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
           q2.push_back({dv3[win], end});
         }
       }
-      N.queue = (capped || N.nd == 7) ? std::vector<std::pair<uint32_t, uint32_t>>{} : q2;
+      N.queue = (capped || N.nd == 7) ? CandQueue{} : q2;
       if (!N.queue.empty()) {
         next.push_back(std::move(N));
         continue;
@@ -909,25 +1091,46 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
         H.emplace_back();
         ranges.push_back(Task{lo / 3, hi / 3});
         range_of.push_back({N.node, c});
-        next.push_back(Open{node.child[c], lo, hi, {{lo, hi}}, {}, 0});
+        next.push_back(Open{node.child[c], lo, hi, CandQueue::of(lo, hi), {}, 0});
       }
       H[N.node] = node;
     }
+    pt.hstop(1);
+    pt.hstart();
     if (T) {
       BVH_DEV(hipMemcpyAsync(dact.p, action.data(), T * 4, hipMemcpyHostToDevice, st), "upload");
-      k_stage_apply<<<T, 256, 0, st>>>(dtasks.p, dact.p, ids3.p, backup.p, n);
+      k_stage_apply<<<NC0, 256, 0, st>>>(dchunks.p, dact.p, ids3.p, backup.p, n);
       BVH_DEV(hipGetLastError(), "stage apply");
     }
     if (ranges.size() > r0) {  // boxes of the children of the nodes completed in this stage
       if (ranges.size() > max_ranges) return hfail("child range bound", hipErrorInvalidValue);
-      const size_t nr = ranges.size() - r0;
-      BVH_DEV(hipMemcpyAsync(dranges.p + r0, ranges.data() + r0, nr * sizeof(Task), hipMemcpyHostToDevice, st),
-              "upload");
-      k_range_box<<<(uint32_t)nr, kSahT, 0, st>>>(dranges.p + r0, ids3.p, tbox.p, boxes.p + r0);
+      const uint32_t nr = (uint32_t)(ranges.size() - r0);
+      rch.clear();
+      rgrp.resize(nr);
+      for (uint32_t r = 0; r < nr; ++r) {
+        const Task &R = ranges[r0 + r];
+        rgrp[r].first = (uint32_t)rch.size();
+        for (uint32_t lo = R.s; lo < R.e; lo += kSahChunk)
+          rch.push_back(SahChunk{r, 0u, lo, std::min<uint32_t>(R.e, lo + kSahChunk), r});
+        rgrp[r].count = (uint32_t)rch.size() - rgrp[r].first;
+      }
+      const uint32_t nrc = (uint32_t)rch.size();
+      if (drch.reserve(nrc) || drgrp.reserve(nr) || rcbox.reserve(nrc)) return fail("allocation");
+      BVH_DEV(hipMemcpyAsync(drch.p, rch.data(), nrc * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(drgrp.p, rgrp.data(), nr * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
+      k_sah_chunk_box<<<nrc, kSahT, 0, st>>>(drch.p, ids3.p, tbox.p, n, rcbox.p);
+      k_group_fold<<<(nr + 63) / 64, 64, 0, st>>>(drgrp.p, nr, rcbox.p, boxes.p + r0);
       BVH_DEV(hipGetLastError(), "child boxes");
+      BVH_DEV(hipStreamSynchronize(st), "child boxes");  // rch / rgrp are reused by the next stage
     }
+    pt.hstop(2);
     open.swap(next);
   }
+  if (pt.on) {
+    (void)hipStreamSynchronize(st);
+    pt.acc[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+  }
+  pt.start();
   // the child boxes, and the final triangle order
   std::vector<uint32_t> cur(n);
   if (!ranges.empty()) {
@@ -942,16 +1145,19 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   }
   BVH_DEV(hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st), "download");
   BVH_DEV(hipStreamSynchronize(st), "download");
+  pt.stop(6);
   pt.start();
-  bvh_layout(vpos4, idx, nidx, H, cur, out, with_canon);
+  bvh_layout(vpos4, idx, nidx, HostNodes(H.p, H.size()), cur, out, with_canon);
   pt.stop(3);
   if (pt.on)
     std::fprintf(stderr,
-                 "[bvh gpu] %u tris: total %.1f ms | alloc+upload %.1f, partition rounds %.1f (%d rounds), serial "
-                 "sorts %.1f (%d launches), SAH %.1f, layout %.1f; %d stages\n",
+                 "[bvh gpu] %u tris: total %.1f ms | alloc+upload+tri boxes %.1f, stages %.1f (partition rounds %.1f "
+                 "(%d rounds), serial sorts %.1f (%d launches), SAH %.1f, other %.1f), boxes+download %.1f, layout "
+                 "%.1f; %d stages; host sections: stage prologue %.1f, FIFO %.1f, apply+boxes %.1f\n",
                  n, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(),
-                 pt.acc[7], pt.acc[0], pt.rounds, pt.acc[1], pt.serial_launches, pt.acc[2], pt.acc[3],
-                 pt.stages);
+                 pt.acc[7], pt.acc[5], pt.acc[0], pt.rounds, pt.acc[1], pt.serial_launches, pt.acc[2],
+                 pt.acc[5] - pt.acc[0] - pt.acc[1] - pt.acc[2], pt.acc[6], pt.acc[3], pt.stages, pt.host[0],
+                 pt.host[1], pt.host[2]);
   return true;
 #undef BVH_DEV
 }

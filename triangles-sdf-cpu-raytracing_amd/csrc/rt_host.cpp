@@ -517,7 +517,7 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
   return true;
 }
 
-void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
+void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, HostNodes H,
                 const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon) {
   const int64_t ntri = nidx / 3;
   out.host_nodes = (int64_t)H.size();
@@ -527,6 +527,7 @@ void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std
   for (int64_t t = 0; t < ntri; ++t)
     for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)cur[t] + k];
   if (with_canon) {  // canonical pre-order (52 u32 per node), same as the oracle's export
+    out.canon.reserve(H.size() * 52);
     std::vector<int32_t> st{0};
     while (!st.empty()) {
       int32_t id = st.back();

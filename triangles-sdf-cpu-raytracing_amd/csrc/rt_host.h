@@ -52,8 +52,18 @@ struct BvhHostNode {
 };
 // libstdc++ std::sort of ids by K[id] (< 0 depth: std::sort's own limit).
 void host_introsort(uint32_t *ids, size_t n, const float *K, int64_t depth_limit);
+// A built tree's nodes, wherever they are stored (std::vector for the host
+// builder, a huge-page arena for the device builder).
+struct HostNodes {
+  const BvhHostNode *p;
+  size_t n;
+  HostNodes(const std::vector<BvhHostNode> &v) : p(v.data()), n(v.size()) {}
+  HostNodes(const BvhHostNode *ptr, size_t count) : p(ptr), n(count) {}
+  size_t size() const { return n; }
+  const BvhHostNode &operator[](size_t i) const { return p[i]; }
+};
 // Canonical export + GPU layout (GNode / GTri, BFS over inner nodes) of a built tree.
-void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, const std::vector<BvhHostNode> &H,
+void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, HostNodes H,
                 const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon = true);
 // The same tree built on the current HIP device (rt_bvhgpu.hip): libstdc++'s
 // introsort replicated with parallel Hoare partitions, SAH sweeps as device
