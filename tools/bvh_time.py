@@ -1,6 +1,8 @@
-"""BVH8 build time (rt_bvh_export = the build + a copy of its export) with the
-host builder and, when a GPU is visible, the device builder (rt_set_bvh_builder):
-bunny and the 1.1M-triangle config-5 stand-in, best of 3.
+"""BVH8 build time with the host builder and, when a GPU is visible, the device
+builder (rt_set_bvh_builder): bunny and the 1.1M-triangle config-5 stand-in,
+best of 3. Two paths: rt_bvh_export (the build and the node count, no
+export arrays) and rt_scene_create_mesh (the build, the GPU layout and the
+scene's device arrays: what a renderer waits for).
 usage: OMP_NUM_THREADS=n python tools/bvh_time.py"""
 import ctypes as C
 import os
@@ -28,6 +30,20 @@ def build_ms(v, i, mode=1):
     return best * 1e3, nn.value
 
 
+def scene_ms(v, i, mode=1):
+    rtamd._lib.check(rtamd.lib().rt_set_bvh_builder(mode))
+    v = np.ascontiguousarray(v, np.float32)
+    i = np.ascontiguousarray(i, np.uint32)
+    best = 1e30
+    for _ in range(3):
+        sc = C.c_void_p()
+        t0 = time.perf_counter()
+        rtamd._lib.check(rtamd.lib().rt_scene_create_mesh(v.ctypes.data, len(v), i.ctypes.data, i.size, C.byref(sc)))
+        best = min(best, time.perf_counter() - t0)
+        rtamd.lib().rt_scene_destroy(sc)
+    return best * 1e3
+
+
 bunny = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
 big = rtamd.subdivide_mesh(bunny, 2)
 thr = os.environ.get("OMP_NUM_THREADS", "default")
@@ -37,3 +53,6 @@ for name, m in (("bunny", bunny), ("bunny x16 (1.1M)", big)):
         ms, n = build_ms(m.vPos4f, m.indices, mode)
         print(f"{label} builder, OMP threads {thr}: {name}: {m.indices.size // 3} tris, {n} nodes, {ms:.1f} ms",
               flush=True)
+        if mode == 2:
+            print(f"  scene creation (build + layout + device arrays), {label} builder: {name}: "
+                  f"{scene_ms(m.vPos4f, m.indices, mode):.1f} ms", flush=True)

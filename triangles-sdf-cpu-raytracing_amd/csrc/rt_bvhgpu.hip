@@ -26,6 +26,7 @@
 // re-sorts its range even when it does not split.
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -38,22 +39,22 @@
 
 #include "../../include/rtamd.h"
 #include "rt_error.h"
+#include "rt_bvhstage.h"
 #include "rt_host.h"
 #include "rt_layout.h"
 
 namespace {
 
+using rth::bvhs::SahChunk;
+using rth::bvhs::SahGroup;
+using rth::bvhs::Seg;
+using rth::bvhs::Task;
+
 #ifndef RT_SERIAL_MAX
 #define RT_SERIAL_MAX 256  // A/B switch
 #endif
 constexpr uint32_t kSerialMax = RT_SERIAL_MAX;  // segments at most this long: one wave, serial introsort in LDS
-constexpr int kScanT = 256, kScanI = 8, kScanBlk = kScanT * kScanI;
 
-struct Seg {
-  uint32_t first, last;  // position range in the 3n-element space (axis a: [a*n, (a+1)*n))
-  int32_t depth;         // remaining introsort depth
-  uint32_t pad;
-};
 
 // ---- libstdc++'s sort algorithms --------------------------------------------
 // On an LDS array of (key, id) pairs compared by key: moving the pairs is
@@ -209,89 +210,79 @@ __global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t *ids, c
   for (uint32_t i = threadIdx.x; i < len; i += 64) ids[s.first + i] = a[i].id;
 }
 
-// ---- inclusive scan of u32 (three launches) --------------------------------
-// blockIdx.y (k_scan1, k_scan3) / blockIdx.x (k_scan2) selects one of two
-// independent arrays, so the partition round's two flag scans share launches
-struct ScanPair {
-  const uint32_t *in[2];
-  uint32_t *out[2];
-  uint32_t *bsum[2];
-};
-__global__ __launch_bounds__(kScanT) void k_scan1(ScanPair sp, uint32_t n) {
-  const uint32_t *in = sp.in[blockIdx.y];
-  uint32_t *out = sp.out[blockIdx.y], *bsum = sp.bsum[blockIdx.y];
-  __shared__ uint32_t sm[kScanT];
-  const uint32_t base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
-  uint32_t v[kScanI], acc = 0;
+// ---- one round of parallel introsort partitions ----------------------------
+// A round is six launches that read the round's segment count m and element
+// count E from device memory (RoundCtl), so the host enqueues several rounds
+// back to back with upper bounds for the grids and synchronises once per batch
+// (a round whose m is 0 exits at once). Element space of a round: the active
+// segments back to back (virtual index v; segment i covers [offs[i], offs[i+1])).
+constexpr int kRoundT = 256, kRoundI = 8, kRoundTile = kRoundT * kRoundI;
+constexpr int kMaxRounds = 64;  // > the introsort depth limit 2 lg2(3n) + 1: a sort never needs more
+// ctl words: [0] serial-list count, [1..3] unused, then (m, E) of round r at [4 + 2 r]
+constexpr int kCtlWords = 4 + 2 * (kMaxRounds + 1);
+
+// exclusive scan of cnt u32 values by one 256-thread block, out[cnt] = total
+// (in == out allowed: each thread reads its values before writing them)
+__device__ void block_excl_scan(const uint32_t *in, uint32_t *out, uint32_t cnt, uint32_t *sm) {
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < cnt; base += kRoundTile) {
+    const uint32_t b0 = base + threadIdx.x * kRoundI;
+    uint32_t v[kRoundI], acc = 0;
 #pragma unroll
-  for (int k = 0; k < kScanI; ++k) {
-    acc += (base + k < n) ? in[base + k] : 0u;
-    v[k] = acc;
-  }
-  sm[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = 1; o < kScanT; o <<= 1) {
-    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
-    __syncthreads();
-    sm[threadIdx.x] += x;
-    __syncthreads();
-  }
-  const uint32_t ex = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
-#pragma unroll
-  for (int k = 0; k < kScanI; ++k)
-    if (base + k < n) out[base + k] = v[k] + ex;
-  if (threadIdx.x == kScanT - 1) bsum[blockIdx.x] = sm[kScanT - 1];
-}
-__global__ __launch_bounds__(1024) void k_scan2(ScanPair sp, uint32_t nb) {
-  uint32_t *bsum = sp.bsum[blockIdx.x];
-  __shared__ uint32_t sm[1024];
-  const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
-  uint32_t acc = 0;
-  for (uint32_t k = 0; k < per; ++k)
-    if (b0 + k < nb) acc += bsum[b0 + k];
-  sm[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
-    __syncthreads();
-    sm[threadIdx.x] += x;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
-  for (uint32_t k = 0; k < per; ++k)
-    if (b0 + k < nb) {
-      run += bsum[b0 + k];
-      bsum[b0 + k] = run;
+    for (int k = 0; k < kRoundI; ++k) {
+      v[k] = acc;
+      acc += (b0 + k < cnt) ? in[b0 + k] : 0u;
     }
-}
-__global__ __launch_bounds__(kScanT) void k_scan3(ScanPair sp, uint32_t n) {
-  uint32_t *out = sp.out[blockIdx.y];
-  const uint32_t *bsum = sp.bsum[blockIdx.y];
-  if (blockIdx.x == 0) return;
-  const uint32_t add = bsum[blockIdx.x - 1], base = blockIdx.x * kScanBlk + threadIdx.x * kScanI;
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 1; o < kRoundT; o <<= 1) {
+      const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sm[threadIdx.x] += x;
+      __syncthreads();
+    }
+    const uint32_t ex = carry + (threadIdx.x ? sm[threadIdx.x - 1] : 0u);
 #pragma unroll
-  for (int k = 0; k < kScanI; ++k)
-    if (base + k < n) out[base + k] += add;
+    for (int k = 0; k < kRoundI; ++k)
+      if (b0 + k < cnt) out[b0 + k] = ex + v[k];
+    carry += sm[kRoundT - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[cnt] = carry;
 }
 
-// ---- one round of parallel introsort partitions ----------------------------
+struct Round {
+  const Seg *cur;
+  Seg *nxt;
+  uint32_t *ctl;
+  int r;  // (m, E) of this round at ctl[4 + 2 r], of the next at ctl[6 + 2 r]
+  __device__ uint32_t m() const { return ctl[4 + 2 * r]; }
+};
+
 // per segment: median to the front, pivot key, size (0: depth exhausted, the
 // segment goes to the serial list, whose introsort loop heapsorts it)
-__global__ void k_prep(const Seg *segs, uint32_t m, uint32_t *ids, const float *K3, uint32_t n, float *kp,
-                       uint32_t *size, Seg *serial, uint32_t *nserial) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const Seg s = segs[i];
-  if (s.depth == 0) {
-    serial[atomicAdd(nserial, 1u)] = s;
-    size[i] = 0;
-    return;
+__global__ __launch_bounds__(kRoundT) void k_prep(Round R, uint32_t *ids, const float *K3, uint32_t n, float *kp,
+                                                  uint32_t *size, uint32_t *sw, Seg *serial) {
+  const uint32_t m = R.m(), i = blockIdx.x * kRoundT + threadIdx.x;
+  if (i < m) {
+    const Seg s = R.cur[i];
+    sw[i] = 0;
+    if (s.depth == 0) {
+      serial[atomicAdd(&R.ctl[0], 1u)] = s;
+      size[i] = 0;
+    } else {
+      const float *K = K3 + (size_t)(s.first / n) * n;
+      uint32_t *f = ids + s.first, *l = ids + s.last;
+      d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
+      kp[i] = K[*f];
+      size[i] = s.last - s.first;
+    }
   }
-  const float *K = K3 + (size_t)(s.first / n) * n;
-  uint32_t *f = ids + s.first, *l = ids + s.last;
-  d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
-  kp[i] = K[*f];
-  size[i] = s.last - s.first;
+}
+// one block: the segment sizes into offs[0..m] (exclusive, offs[m] = E)
+__global__ __launch_bounds__(kRoundT) void k_scan_sizes(Round R, const uint32_t *size, uint32_t *offs) {
+  __shared__ uint32_t sm[kRoundT];
+  block_excl_scan(size, offs, R.m(), sm);
 }
 
 __device__ __forceinline__ uint32_t seg_of(const uint32_t *offs, uint32_t m, uint32_t v) {
@@ -304,100 +295,166 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t *offs, uint32_t m, uin
   return lo;
 }
 
-// flags over the active elements (virtual index v, segments back to back):
+// Prefix counts of the two flag kinds over the round's elements:
 // a = stops the left scan of the partition (!(key < pivot), the pivot itself
-// excluded), b = stops the right scan (!(pivot < key), the pivot included)
-__global__ void k_flags(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *ids, const float *K3,
-                        uint32_t n, const float *kp, uint32_t *af, uint32_t *bf, uint32_t *segv, uint32_t E) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= E || v >= offs[m]) return;  // E: host bound; offs[m]: elements of this round
-  const uint32_t i = seg_of(offs, m, v);
-  const Seg s = segs[i];
-  const uint32_t p = s.first + (v - offs[i]);
-  const float *K = K3 + (size_t)(s.first / n) * n;
-  const float k = K[ids[p]], pk = kp[i];
-  af[v] = (p != s.first && !(k < pk)) ? 1u : 0u;
-  bf[v] = (p == s.first || !(pk < k)) ? 1u : 0u;
-  segv[v] = i;
+// excluded), b = stops the right scan (!(pivot < key), the pivot included).
+// Per tile of kRoundTile elements the in-tile inclusive counts (Aloc / Bloc),
+// the tile totals (exclusive-scanned over the tiles by k_scan_tiles), and
+// per segment the in-tile count before its first element (startA / startB)
+// and through its last (endA / endB). Global inclusive count at v:
+// tileA[v / tile] + Aloc[v].
+struct Prefix {
+  uint32_t *Aloc, *Bloc, *tileA, *tileB, *startA, *startB, *endA, *endB;
+  __device__ uint32_t a_at(uint32_t v) const { return tileA[v / kRoundTile] + Aloc[v]; }
+  __device__ uint32_t b_at(uint32_t v) const { return tileB[v / kRoundTile] + Bloc[v]; }
+  // a / b elements before segment i (o = its first element) and through it (oe = one past its last)
+  __device__ uint32_t a_before(uint32_t i, uint32_t o) const { return tileA[o / kRoundTile] + startA[i]; }
+  __device__ uint32_t b_before(uint32_t i, uint32_t o) const { return tileB[o / kRoundTile] + startB[i]; }
+  __device__ uint32_t a_through(uint32_t i, uint32_t oe) const { return tileA[(oe - 1) / kRoundTile] + endA[i]; }
+  __device__ uint32_t b_through(uint32_t i, uint32_t oe) const { return tileB[(oe - 1) / kRoundTile] + endB[i]; }
+};
+
+__global__ __launch_bounds__(kRoundT) void k_flags(Round R, const uint32_t *offs, const uint32_t *ids,
+                                                   const float *K3, uint32_t n, const float *kp, uint8_t *fl,
+                                                   uint32_t *segv, Prefix P) {
+  __shared__ uint32_t sm[kRoundT];
+  const uint32_t m = R.m(), E = offs[m];
+  if (blockIdx.x * kRoundTile >= E) return;
+  const uint32_t b0 = blockIdx.x * kRoundTile + threadIdx.x * kRoundI;
+  uint32_t f[kRoundI], cnt = 0;  // packed counts: a in bits 0-15, b in 16-31 (<= 2048 each per tile)
+  uint32_t i = b0 < E ? seg_of(offs, m, b0) : 0;
+#pragma unroll
+  for (int k = 0; k < kRoundI; ++k) {
+    const uint32_t v = b0 + k;
+    f[k] = 0;
+    if (v < E) {
+      while (offs[i + 1] <= v) ++i;  // zero-size segments (serial) are skipped
+      const Seg s = R.cur[i];
+      const uint32_t p = s.first + (v - offs[i]);
+      const float key = K3[(size_t)(s.first / n) * n + ids[p]], pk = kp[i];
+      f[k] = ((p != s.first && !(key < pk)) ? 1u : 0u) | ((p == s.first || !(pk < key)) ? 0x10000u : 0u);
+      segv[v] = i;
+      fl[v] = (uint8_t)((f[k] & 1u) | (f[k] >> 15));
+    }
+    cnt += f[k];
+  }
+  sm[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = 1; o < kRoundT; o <<= 1) {
+    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sm[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
+  i = b0 < E ? seg_of(offs, m, b0) : 0;
+#pragma unroll
+  for (int k = 0; k < kRoundI; ++k) {
+    const uint32_t v = b0 + k;
+    if (v < E) {
+      while (offs[i + 1] <= v) ++i;
+      if (v == offs[i]) {
+        P.startA[i] = run & 0xFFFFu;
+        P.startB[i] = run >> 16;
+      }
+      run += f[k];
+      P.Aloc[v] = run & 0xFFFFu;
+      P.Bloc[v] = run >> 16;
+      if (v + 1 == offs[i + 1]) {
+        P.endA[i] = run & 0xFFFFu;
+        P.endB[i] = run >> 16;
+      }
+    }
+  }
+  if (threadIdx.x == kRoundT - 1) {
+    P.tileA[blockIdx.x] = sm[kRoundT - 1] & 0xFFFFu;
+    P.tileB[blockIdx.x] = sm[kRoundT - 1] >> 16;
+  }
+}
+// one block: the tile totals into exclusive prefixes
+__global__ __launch_bounds__(kRoundT) void k_scan_tiles(Round R, const uint32_t *offs, Prefix P) {
+  __shared__ uint32_t sm[kRoundT];
+  const uint32_t nt = (offs[R.m()] + kRoundTile - 1) / kRoundTile;
+  block_excl_scan(P.tileA, P.tileA, nt, sm);
+  block_excl_scan(P.tileB, P.tileB, nt, sm);
 }
 
 // ranks of the a-elements from the left and the b-elements from the right,
-// scattered into per-segment position lists L, R (v-space, offs[i] + rank - 1)
-__global__ void k_ranks(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af, const uint32_t *bf,
-                        const uint32_t *Ai, const uint32_t *Bi, const uint32_t *segv, uint32_t *Lpos,
-                        uint32_t *Rpos, uint32_t E) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= E || v >= offs[m]) return;
-  const uint32_t i = segv[v], o = offs[i], oe = offs[i + 1];
-  const uint32_t p = segs[i].first + (v - o);
-  const uint32_t abase = o ? Ai[o - 1] : 0u, bbase = o ? Bi[o - 1] : 0u;
-  if (af[v]) Lpos[o + (Ai[v] - abase) - 1] = p;
-  if (bf[v]) {
-    const uint32_t btot = Bi[oe - 1] - bbase;
-    Rpos[o + (btot - (Bi[v] - bbase) + 1) - 1] = p;
+// scattered into per-segment position lists L, R (v-space, offs[i] + rank - 1),
+// and the number of swaps: the a-element of rank k swaps with the b-element of
+// rank k from the right while it lies left of it, i.e. while at least k
+// b-elements lie strictly right of it -- monotone in k, so the swap count is
+// the number of a-elements for which it holds (summed per wave)
+__global__ __launch_bounds__(kRoundT) void k_ranks(Round R, const uint32_t *offs, const uint8_t *fl,
+                                                   const uint32_t *segv, Prefix P, uint32_t *Lpos, uint32_t *Rpos,
+                                                   uint32_t *sw) {
+  const uint32_t m = R.m(), E = offs[m];
+  const uint32_t v = blockIdx.x * kRoundT + threadIdx.x;
+  const bool live = v < E;
+  uint32_t i = 0;
+  bool swaps = false;
+  if (live) {
+    i = segv[v];
+    const uint32_t o = offs[i], oe = offs[i + 1], p = R.cur[i].first + (v - o);
+    const uint8_t f = fl[v];
+    if (f & 1u) {
+      const uint32_t rank = P.a_at(v) - P.a_before(i, o);
+      Lpos[o + rank - 1] = p;
+      swaps = P.b_through(i, oe) - P.b_at(v) >= rank;  // b-elements strictly right of p
+    }
+    if (f & 2u) {
+      const uint32_t btot = P.b_through(i, oe) - P.b_before(i, o), rank = P.b_at(v) - P.b_before(i, o);
+      Rpos[o + (btot - rank)] = p;
+    }
+  }
+  const uint64_t act = __ballot(live);
+  if (act == 0) return;
+  const uint32_t i0 = (uint32_t)__shfl(i, __ffsll((unsigned long long)act) - 1);
+  if (__ballot(live && i != i0) == 0) {  // one segment in this wave: one atomic
+    const uint32_t c = (uint32_t)__popcll(__ballot(swaps));
+    if (c && (int)(threadIdx.x & 63u) == __ffsll((unsigned long long)act) - 1) atomicAdd(&sw[i0], c);
+  } else if (swaps) {
+    atomicAdd(&sw[i], 1u);
   }
 }
 
-// number of swaps s: the a-element of rank k swaps with the b-element of rank
-// k from the right while it lies left of it, i.e. while at least k b-elements
-// lie strictly right of it (monotone in k); the a-element where that stops
-// writes s (one writer per segment; s stays 0 if the first one fails)
-__device__ __forceinline__ bool pred_at(const Seg &s, uint32_t o, uint32_t oe, uint32_t p, uint32_t rank,
-                                        const uint32_t *Bi) {
-  const uint32_t v = o + (p - s.first);
-  const uint32_t nright = Bi[oe - 1] - Bi[v];  // b-elements strictly right of p
-  return nright >= rank;
-}
-__global__ void k_swaps_count(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af,
-                              const uint32_t *Ai, const uint32_t *Bi, const uint32_t *segv, const uint32_t *Lpos,
-                              uint32_t *sw, uint32_t E) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= E || v >= offs[m] || !af[v]) return;
-  const uint32_t i = segv[v], o = offs[i], oe = offs[i + 1];
-  const Seg s = segs[i];
-  const uint32_t abase = o ? Ai[o - 1] : 0u, na = Ai[oe - 1] - abase, rank = Ai[v] - abase;
-  const uint32_t p = s.first + (v - o);
-  if (!pred_at(s, o, oe, p, rank, Bi)) return;
-  if (rank == na || !pred_at(s, o, oe, Lpos[o + rank], rank + 1, Bi)) sw[i] = rank;
-}
-
-// the swaps themselves: one thread per pair (its a-element)
-__global__ void k_swap(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *af, const uint32_t *Ai,
-                       const uint32_t *segv, const uint32_t *Rpos, const uint32_t *sw, uint32_t *ids, uint32_t E) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= E || v >= offs[m] || !af[v]) return;
-  const uint32_t i = segv[v], o = offs[i];
-  const uint32_t rank = Ai[v] - (o ? Ai[o - 1] : 0u);
-  if (rank > sw[i]) return;
-  const uint32_t p = segs[i].first + (v - o), q = Rpos[o + rank - 1];
-  const uint32_t t = ids[p];
-  ids[p] = ids[q];
-  ids[q] = t;
-}
-
-// the cut (where the left scan stops after the last swap) and the two parts:
-// longer than kSerialMax -> next round, else the serial list
-__global__ void k_split(const Seg *segs, const uint32_t *offs, uint32_t m, const uint32_t *size, const uint32_t *Ai,
-                        const uint32_t *Lpos, const uint32_t *Rpos, const uint32_t *sw, Seg *next,
-                        uint32_t *nnext, uint32_t *Enext, Seg *serial, uint32_t *nserial) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m || size[i] == 0) return;
-  const Seg s = segs[i];
-  const uint32_t o = offs[i], oe = offs[i + 1];
-  const uint32_t na = Ai[oe - 1] - (o ? Ai[o - 1] : 0u), k = sw[i];
+// the swaps (one thread per pair: its a-element) and, per segment, the cut
+// (where the left scan stops after the last swap) and the two parts: longer
+// than kSerialMax -> the next round, else the serial list
+__global__ __launch_bounds__(kRoundT) void k_swap_split(Round R, const uint32_t *offs, const uint32_t *size,
+                                                        const uint8_t *fl, const uint32_t *segv, Prefix P,
+                                                        const uint32_t *Lpos, const uint32_t *Rpos,
+                                                        const uint32_t *sw, uint32_t *ids, Seg *serial) {
+  const uint32_t m = R.m(), E = offs[m];
+  const uint32_t t = blockIdx.x * kRoundT + threadIdx.x;
+  if (t < E && (fl[t] & 1u)) {
+    const uint32_t i = segv[t], o = offs[i];
+    const uint32_t rank = P.a_at(t) - P.a_before(i, o);
+    if (rank <= sw[i]) {
+      const uint32_t p = R.cur[i].first + (t - o), q = Rpos[o + rank - 1];
+      const uint32_t x = ids[p];
+      ids[p] = ids[q];
+      ids[q] = x;
+    }
+  }
+  if (t >= m || size[t] == 0) return;
+  const Seg s = R.cur[t];
+  const uint32_t o = offs[t], oe = offs[t + 1];
+  const uint32_t na = P.a_through(t, oe) - P.a_before(t, o), k = sw[t];
   uint32_t cut;
   if (k == 0) cut = Lpos[o];  // the median of three guarantees an element >= pivot
   else {
     const uint32_t rk = Rpos[o + k - 1];
     cut = (k < na) ? min(Lpos[o + k], rk) : rk;
   }
+  uint32_t *next_mE = R.ctl + 6 + 2 * R.r;
   const Seg parts[2] = {Seg{cut, s.last, s.depth - 1, 0}, Seg{s.first, cut, s.depth - 1, 0}};
   for (const Seg &q : parts) {
     if (q.last - q.first > kSerialMax) {
-      next[atomicAdd(nnext, 1u)] = q;
-      atomicAdd(Enext, q.last - q.first);
+      R.nxt[atomicAdd(&next_mE[0], 1u)] = q;
+      atomicAdd(&next_mE[1], q.last - q.first);
     } else if (q.last - q.first > 1) {
-      serial[atomicAdd(nserial, 1u)] = q;
+      serial[atomicAdd(&R.ctl[0], 1u)] = q;
     }
   }
 }
@@ -445,9 +502,6 @@ __device__ TBox block_excl_box(const TBox &b, TBox *sm, TBox *tot) {
   return ex;
 }
 
-struct Task {
-  uint32_t s, e;  // triangle range [s, e) of one candidate
-};
 
 // ---- SAH sweeps over chunks: many workgroups per (candidate, axis) ----------
 // The sweep above walks a whole candidate range in ONE workgroup, so the top
@@ -460,13 +514,6 @@ struct Task {
 // the prefix -- and the chunk's first minimum; the host takes the first
 // minimum over the chunks. Box unions are exact min / max, so the areas, and
 // with them every cost, are the sequential sweep's values.
-struct SahChunk {
-  uint32_t task, axis, lo, hi;  // triangle range [lo, hi) of candidate `task` on `axis`
-  uint32_t group;               // task * 3 + axis
-};
-struct SahGroup {
-  uint32_t first, count;  // its chunks
-};
 
 __global__ __launch_bounds__(kSahT) void k_sah_chunk_box(const SahChunk *chunks, const uint32_t *ids3,
                                                          const TBox *tbox, uint32_t n, TBox *cbox) {
@@ -636,6 +683,34 @@ __global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TB
   K3[2 * n + t] = b.mx[2];
 }
 
+// the leaf triangles in slot order (bvh_layout's fill_tris, rt_host.cpp; the
+// vertices /= w as triangles_raytracing.cpp:307-309): one thread per leaf,
+// tab = (first slot, first position in the final order, count)
+__global__ void k_fill_tris(const uint32_t *tab, uint32_t nl, const float4 *vpos, const uint32_t *idx,
+                            const uint32_t *order, rtl::GTri *tris) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  const uint32_t first = tab[3 * l], pos = tab[3 * l + 1], cnt = tab[3 * l + 2];
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint32_t id = order[pos + k];
+    float v[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float4 p = vpos[idx[3 * id + j]];
+      v[j][0] = p.x / p.w;
+      v[j][1] = p.y / p.w;
+      v[j][2] = p.z / p.w;
+    }
+    rtl::GTri g;
+    g.v0x = v[0][0]; g.v0y = v[0][1]; g.v0z = v[0][2];
+    g.orig_id = id;
+    g.e1x = v[1][0] - v[0][0]; g.e1y = v[1][1] - v[0][1]; g.e1z = v[1][2] - v[0][2];
+    g.e2x = v[2][0] - v[0][0]; g.e2y = v[2][1] - v[0][1]; g.e2z = v[2][2] - v[0][2];
+    g.pad1 = g.pad2 = 0.0f;
+    tris[first + k] = g;
+  }
+}
+
 // ---- host side ---------------------------------------------------------------
 // RTAMD_BVH_TIMING=1: per-phase wall time of a device build on stderr (the
 // phases are synchronised for the measurement)
@@ -643,9 +718,22 @@ struct PhaseTimer {
   bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
   double acc[8] = {};
   double host[4] = {};  // wall time of host-side stage sections (no syncs): prologue, FIFO, apply+boxes
+  long faults[4] = {};  // minor page faults in those sections
   std::chrono::steady_clock::time_point h0;
-  void hstart() { h0 = std::chrono::steady_clock::now(); }
-  void hstop(int k) { host[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); }
+  long f0 = 0;
+  static long minflt() {
+    rusage u;
+    getrusage(RUSAGE_THREAD, &u);
+    return u.ru_minflt;
+  }
+  void hstart() {
+    h0 = std::chrono::steady_clock::now();
+    if (on) f0 = minflt();
+  }
+  void hstop(int k) {
+    host[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    if (on) faults[k] += minflt() - f0;
+  }
   int rounds = 0, stages = 0, serial_launches = 0;
   std::chrono::steady_clock::time_point t0;
   hipStream_t st = nullptr;
@@ -693,9 +781,10 @@ struct Sorter {
   uint32_t *ids = nullptr;
   const float *K3 = nullptr;
   DBuf<Seg> segA, segB, serial;
-  DBuf<uint32_t> size, offs, sw, af, bf, Ai, Bi, segv, Lpos, Rpos, bsum, ctr;
+  DBuf<uint32_t> size, offs, sw, Aloc, Bloc, tiles, bnd, segv, Lpos, Rpos, ctl;
+  DBuf<uint8_t> fl;
   DBuf<float> kp;
-  size_t bsum_half = 0;  // bsum: two halves, one per array of a paired scan
+  size_t segcap = 0, tilecap = 0;
   hipStream_t st = nullptr;
   PhaseTimer own_pt;             // per build: concurrent builds share no state
   PhaseTimer *pt = &own_pt;
@@ -704,75 +793,74 @@ struct Sorter {
     n = ntri;
     ids = ids3;
     K3 = keys3;
-    const size_t N = 3 * (size_t)n, segcap = N / kSerialMax + 16, sercap = N / 2 + 4096;
+    const size_t N = 3 * (size_t)n, sercap = N / 2 + 4096;
+    segcap = N / (kSerialMax + 1) + 16;
+    tilecap = N / kRoundTile + 2;
     int rc;
     if ((rc = segA.reserve(segcap)) || (rc = segB.reserve(segcap)) || (rc = serial.reserve(sercap)) ||
         (rc = size.reserve(segcap + 1)) || (rc = offs.reserve(segcap + 1)) || (rc = sw.reserve(segcap)) ||
-        (rc = kp.reserve(segcap)) || (rc = af.reserve(N)) || (rc = bf.reserve(N)) || (rc = Ai.reserve(N)) ||
-        (rc = Bi.reserve(N)) || (rc = segv.reserve(N)) || (rc = Lpos.reserve(N)) || (rc = Rpos.reserve(N)) ||
-        (rc = bsum.reserve(2 * (N / kScanBlk + 2))) || (rc = ctr.reserve(4)))
+        (rc = kp.reserve(segcap)) || (rc = Aloc.reserve(N)) || (rc = Bloc.reserve(N)) || (rc = fl.reserve(N)) ||
+        (rc = tiles.reserve(2 * tilecap)) || (rc = bnd.reserve(4 * segcap)) || (rc = segv.reserve(N)) ||
+        (rc = Lpos.reserve(N)) || (rc = Rpos.reserve(N)) || (rc = ctl.reserve(kCtlWords)))
       return rc;
-    bsum_half = N / kScanBlk + 2;
-    return RT_OK;
-  }
-
-  // inclusive scans of one array (in1 == nullptr) or of two at once
-  int scan(const uint32_t *in, uint32_t *out, uint32_t cnt, const uint32_t *in1 = nullptr,
-           uint32_t *out1 = nullptr) {
-    if (cnt == 0) return RT_OK;
-    const uint32_t nb = (cnt + kScanBlk - 1) / kScanBlk, na = in1 ? 2u : 1u;
-    const ScanPair sp{{in, in1}, {out, out1}, {bsum.p, bsum.p + bsum_half}};
-    k_scan1<<<dim3(nb, na), kScanT, 0, st>>>(sp, cnt);
-    if (nb > 1) {
-      k_scan2<<<na, 1024, 0, st>>>(sp, nb);
-      k_scan3<<<dim3(nb, na), kScanT, 0, st>>>(sp, cnt);
-    }
-    HIP_TRY(hipGetLastError());
     return RT_OK;
   }
 
   // sort every segment of `init` (host list): exactly std::sort on each
   int sort(const std::vector<Seg> &init) {
     std::vector<Seg> act, ser;
+    uint32_t maxlen = 0;
     for (const Seg &s : init) {
       if (s.last - s.first <= 1) continue;
       (s.last - s.first > kSerialMax ? act : ser).push_back(s);
+      if (s.last - s.first > kSerialMax) maxlen = std::max(maxlen, s.last - s.first);
     }
-    uint32_t nser = (uint32_t)ser.size(), m = (uint32_t)act.size(), E = 0;
+    uint32_t m = (uint32_t)act.size(), E = 0;
     for (const Seg &s : act) E += s.last - s.first;
-    if (nser) HIP_TRY(hipMemcpyAsync(serial.p, ser.data(), nser * sizeof(Seg), hipMemcpyHostToDevice, st));
+    if (m > segcap || ser.size() > serial.cap) return rterr::set(RT_E_DEVICE, "sort: segment list bound");
+    uint32_t hc[kCtlWords] = {};
+    hc[0] = (uint32_t)ser.size();
+    hc[4] = m;
+    hc[5] = E;
+    if (!ser.empty()) HIP_TRY(hipMemcpyAsync(serial.p, ser.data(), ser.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
     if (m) HIP_TRY(hipMemcpyAsync(segA.p, act.data(), m * sizeof(Seg), hipMemcpyHostToDevice, st));
-    uint32_t hc[3] = {0, 0, nser};  // next count, next E, serial count
-    HIP_TRY(hipMemcpyAsync(ctr.p + 2, &hc[2], 4, hipMemcpyHostToDevice, st));
-    Seg *cur = segA.p, *nxt = segB.p;
+    HIP_TRY(hipMemcpyAsync(ctl.p, hc, sizeof(hc), hipMemcpyHostToDevice, st));
+    const Prefix P{Aloc.p, Bloc.p, tiles.p, tiles.p + tilecap, bnd.p, bnd.p + segcap, bnd.p + 2 * segcap,
+                   bnd.p + 3 * segcap};
     pt->start();
-    while (m > 0) {
-      ++pt->rounds;
-      HIP_TRY(hipMemsetAsync(ctr.p, 0, 8, st));
-      HIP_TRY(hipMemsetAsync(sw.p, 0, (size_t)m * 4, st));
-      const uint32_t gm = (m + 255) / 256;
-      k_prep<<<gm, 256, 0, st>>>(cur, m, ids, K3, n, kp.p, size.p + 1, serial.p, ctr.p + 2);
-      HIP_TRY(hipMemsetAsync(size.p, 0, 4, st));
-      if (int rc = scan(size.p, offs.p, m + 1)) return rc;  // offs[i] = sum of sizes before segment i
-      const uint32_t ge = (E + 255) / 256;
-      if (E) {
-        k_flags<<<ge, 256, 0, st>>>(cur, offs.p, m, ids, K3, n, kp.p, af.p, bf.p, segv.p, E);
-        if (int rc = scan(af.p, Ai.p, E, bf.p, Bi.p)) return rc;
-        k_ranks<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, bf.p, Ai.p, Bi.p, segv.p, Lpos.p, Rpos.p, E);
-        k_swaps_count<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, Bi.p, segv.p, Lpos.p, sw.p, E);
-        k_swap<<<ge, 256, 0, st>>>(cur, offs.p, m, af.p, Ai.p, segv.p, Rpos.p, sw.p, ids, E);
-        k_split<<<gm, 256, 0, st>>>(cur, offs.p, m, size.p + 1, Ai.p, Lpos.p, Rpos.p, sw.p, nxt, ctr.p, ctr.p + 1,
-                                    serial.p, ctr.p + 2);
+    // rounds are enqueued in batches, with grid bounds: E never grows, m at
+    // most doubles and each active segment holds more than kSerialMax elements;
+    // the first batch is the round count of even splits of the longest segment
+    int r = 0, batch = m ? std::max(1, lg2(maxlen / kSerialMax) + 1) : 0;
+    uint32_t mb = m, Eb = E;
+    while (mb > 0) {
+      for (int b = 0; b < batch && mb > 0; ++b, ++r) {
+        if (r >= kMaxRounds) return rterr::set(RT_E_DEVICE, "sort: partition round bound");
+        ++pt->rounds;
+        const Round R{(r & 1) ? segB.p : segA.p, (r & 1) ? segA.p : segB.p, ctl.p, r};
+        const uint32_t gm = (mb + kRoundT - 1) / kRoundT, gt = (Eb + kRoundTile - 1) / kRoundTile,
+                       ge = (std::max(Eb, mb) + kRoundT - 1) / kRoundT;
+        k_prep<<<gm, kRoundT, 0, st>>>(R, ids, K3, n, kp.p, size.p, sw.p, serial.p);
+        k_scan_sizes<<<1, kRoundT, 0, st>>>(R, size.p, offs.p);
+        k_flags<<<gt, kRoundT, 0, st>>>(R, offs.p, ids, K3, n, kp.p, fl.p, segv.p, P);
+        k_scan_tiles<<<1, kRoundT, 0, st>>>(R, offs.p, P);
+        k_ranks<<<ge, kRoundT, 0, st>>>(R, offs.p, fl.p, segv.p, P, Lpos.p, Rpos.p, sw.p);
+        k_swap_split<<<ge, kRoundT, 0, st>>>(R, offs.p, size.p, fl.p, segv.p, P, Lpos.p, Rpos.p, sw.p, ids,
+                                             serial.p);
+        HIP_TRY(hipGetLastError());
+        mb = std::min<uint64_t>(2ull * mb, Eb / (kSerialMax + 1));
       }
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(hc, ctr.p, 12, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(hc, ctl.p, (size_t)(6 + 2 * r) * 4, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      m = hc[0];
-      E = hc[1];
-      std::swap(cur, nxt);
+      mb = hc[4 + 2 * r];
+      Eb = hc[5 + 2 * r];
+      batch = 2;
     }
-    HIP_TRY(hipMemcpyAsync(&nser, ctr.p + 2, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (r == 0) {
+      HIP_TRY(hipMemcpyAsync(hc, ctl.p, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    const uint32_t nser = hc[0];
     pt->stop(0);
     pt->start();
     if (nser) k_serial<<<nser, 64, 0, st>>>(serial.p, ids, K3, n);
@@ -783,69 +871,12 @@ struct Sorter {
   }
 };
 
-// The device build's host-side node array (createNode's m_nodes). Up to 2n - 1
-// nodes of ~240 B are written once each as the build proceeds; backed by an
-// anonymous mapping of that bound with transparent huge pages requested, so a
-// 1.1 M-triangle build's ~40 MB of nodes are ~20 page faults instead of ~10^4
-// (untouched pages of the reservation cost nothing).
-struct NodeArena {
-  rth::BvhHostNode *p = nullptr;
-  size_t n = 0, cap = 0, bytes = 0;
-  NodeArena() = default;
-  NodeArena(const NodeArena &) = delete;
-  NodeArena &operator=(const NodeArena &) = delete;
-  ~NodeArena() {
-    if (p) munmap(p, bytes);
-  }
-  bool reserve(size_t c) {
-    const size_t huge = (size_t)2 << 20;
-    bytes = (c * sizeof(rth::BvhHostNode) + huge - 1) / huge * huge;
-    void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (m == MAP_FAILED) return false;
-    (void)madvise(m, bytes, MADV_HUGEPAGE);
-    p = static_cast<rth::BvhHostNode *>(m);
-    cap = c;
-    return true;
-  }
-  size_t size() const { return n; }
-  rth::BvhHostNode &operator[](size_t i) { return p[i]; }
-  void emplace_back() { new (p + n++) rth::BvhHostNode(); }  // n < cap: at most 2 ntri - 1 nodes
-};
-
-// createNode's ChipQueue contents (FIFO). A node splits at most 7 times and
-// its queue is dropped at the 7th split, so it never holds more than 8
-// candidates (a layer of 4 that all split reaches 7 splits); kept inline, so
-// the ~10^5 open nodes of a large build allocate nothing
-struct CandQueue {
-  std::pair<uint32_t, uint32_t> a[16];
-  uint32_t n = 0;
-  const std::pair<uint32_t, uint32_t> *begin() const { return a; }
-  const std::pair<uint32_t, uint32_t> *end() const { return a + n; }
-  size_t size() const { return n; }
-  bool empty() const { return n == 0; }
-  const std::pair<uint32_t, uint32_t> &operator[](size_t i) const { return a[i]; }
-  void push_back(std::pair<uint32_t, uint32_t> c) { a[n < 16 ? n++ : 15] = c; }
-  static CandQueue of(uint32_t lo, uint32_t hi) {
-    CandQueue q;
-    q.push_back({lo, hi});
-    return q;
-  }
-};
-// BVHBuilder::createNode state of one node (triangles_raytracing.cpp:155-225)
-struct Open {
-  int32_t node;
-  uint32_t start, end;  // index units
-  CandQueue queue;
-  uint32_t div[8];
-  int nd = 0;
-};
-
 }  // namespace
 
 namespace rth {
 
 bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                    std::string &err, bool with_canon) {
+                    std::string &err, unsigned want) {
   // every device-side failure is reported as "GPU BVH build: <step>: <HIP
   // error>" (RT_E_DEVICE at the C ABI; in AUTO mode the host builder takes
   // over); input errors carry no prefix (RT_E_INVALID)
@@ -878,15 +909,15 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   PhaseTimer pt;
   pt.start();
   DBuf<float4> dv;
-  DBuf<uint32_t> didx, ids3, backup, ddiv, dact;
-  DBuf<float> K3, dcost;
+  DBuf<uint32_t> didx, ids3, backup, dact;
+  DBuf<float> K3;
   DBuf<TBox> tbox, boxes, cbox, cpre, csuf;
   DBuf<Task> dtasks;
   DBuf<SahChunk> dchunks, drch;
   DBuf<SahGroup> dgroups, drgrp;
   DBuf<TBox> rcbox;
-  std::vector<SahChunk> ch, rch;  // per-stage chunk tables (host copies)
-  std::vector<SahGroup> grp, rgrp;
+  std::vector<SahChunk> rch;  // per-stage child-box chunk table (host copy)
+  std::vector<SahGroup> rgrp;
   uint32_t NC = 0, NC0 = 0;
   DBuf<float> ccost, dpsa;
   DBuf<uint32_t> cdivv;
@@ -915,83 +946,37 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   BVH_DEV(hipGetLastError(), "triangle boxes");
   pt.stop(7);  // allocation, upload, triangle boxes
 
-  // host state reused across the stages (cleared, never freed: fresh pages
-  // of per-stage vectors cost more than the stage logic itself)
-  NodeArena H;
-  if (!H.reserve(2 * (size_t)n + 1)) return hfail("node arena", hipErrorOutOfMemory);
-  H.emplace_back();
-  std::vector<Open> open, next;
-  std::vector<Task> tasks;
-  std::vector<int> task_of;
-  std::vector<uint32_t> task_off, dvd, action;
-  std::vector<float> cost, hcc;
+  // host side of the stages (rt_bvhstage.cpp): nodes, per-node FIFO state,
+  // open lists, child ranges. A node's child boxes are computed in the stage
+  // that completes the node, over the triangle order at that point (calc_bbox
+  // at creation, triangles_raytracing.cpp:199), before the children's own
+  // sorts reorder their ranges (first-kept among equal bounds, so -0.0 / +0.0
+  // come out as the reference's sequential min / max)
+  bvhs::Stage SG;
+  if (!SG.init(n, kSahChunk)) return hfail("host arrays", hipErrorOutOfMemory);
+  if (boxes.reserve(SG.ranges.cap)) return fail("allocation");
+  std::vector<float> hcc;
   std::vector<uint32_t> hcd;
-  std::vector<Seg> segs;
-  open.push_back(Open{0, 0, 3 * n, CandQueue::of(0u, 3 * n), {}, 0});
-  // child ranges (triangle units) and their boxes: a node's child boxes are
-  // computed in the stage that completes the node, over the triangle order at
-  // that point (calc_bbox at creation, triangles_raytracing.cpp:199), before
-  // the children's own sorts reorder their ranges (first-kept among equal
-  // bounds, so -0.0 / +0.0 come out as the reference's sequential min / max)
-  std::vector<Task> ranges;
-  std::vector<std::pair<int32_t, int>> range_of;  // (node, child slot) per range
-  const size_t max_ranges = 2 * (size_t)n + 8;    // every node but the root is a child range
-  ranges.reserve(max_ranges);
-  range_of.reserve(max_ranges);
-  if (boxes.reserve(max_ranges)) return fail("allocation");
   const auto ts0 = std::chrono::steady_clock::now();
-  while (!open.empty()) {
+  while (SG.n_open) {
     ++pt.stages;
     pt.hstart();
-    const size_t r0 = ranges.size();
-    // this stage: every queued candidate of every open node that tryDivide sorts (> 8 triangles)
-    tasks.clear();
-    // task index of open node o's candidate c: task_of[task_off[o] + c] (-1: not sorted)
-    task_of.clear();
-    task_off.resize(open.size());
-    for (size_t o = 0; o < open.size(); ++o) {
-      task_off[o] = (uint32_t)task_of.size();
-      for (auto &c : open[o].queue) {
-        const bool gpu = c.second - c.first > 24;
-        task_of.push_back(gpu ? (int)tasks.size() : -1);
-        if (gpu) tasks.push_back(Task{c.first / 3, c.second / 3});
-      }
-    }
-    const uint32_t T = (uint32_t)tasks.size();
-    cost.assign(3 * (size_t)T, 0.0f);
-    dvd.assign(3 * (size_t)T, 0u);
-    action.assign(T, 0u);
+    const size_t r0 = SG.n_ranges;
+    SG.prologue();
+    const uint32_t T = (uint32_t)SG.tasks.size();
     if (T) {
-      if (dtasks.reserve(T) || dcost.reserve(3 * (size_t)T) || ddiv.reserve(3 * (size_t)T) || dact.reserve(T))
-        return fail("allocation");
-      BVH_DEV(hipMemcpyAsync(dtasks.p, tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st), "upload");
-      // chunks of every (candidate, axis) range: [axis-0 chunks of all candidates | axis 1 | axis 2]
-      ch.clear();
-      grp.assign(3 * (size_t)T, SahGroup{});
-      for (uint32_t a = 0; a < 3; ++a)
-        for (uint32_t ti = 0; ti < T; ++ti) {
-          SahGroup &G = grp[3 * ti + a];
-          G.first = (uint32_t)ch.size();
-          for (uint32_t lo = tasks[ti].s; lo < tasks[ti].e; lo += kSahChunk)
-            ch.push_back(SahChunk{ti, a, lo, std::min<uint32_t>(tasks[ti].e, lo + kSahChunk), 3 * ti + a});
-          G.count = (uint32_t)ch.size() - G.first;
-        }
-      NC = (uint32_t)ch.size();
-      NC0 = NC / 3;  // the axis-0 chunks come first
+      NC = (uint32_t)SG.ch.size();
+      NC0 = SG.nc_axis;  // the axis-0 chunks come first
       const uint32_t NG = 3 * T;
-      if (dchunks.reserve(NC) || dgroups.reserve(NG) || cbox.reserve(NC) || cpre.reserve(NC) || csuf.reserve(NC) ||
-          ccost.reserve(NC) || cdivv.reserve(NC) || dpsa.reserve(NG))
+      if (dtasks.reserve(T) || dact.reserve(T) || dchunks.reserve(NC) || dgroups.reserve(NG) || cbox.reserve(NC) ||
+          cpre.reserve(NC) || csuf.reserve(NC) || ccost.reserve(NC) || cdivv.reserve(NC) || dpsa.reserve(NG))
         return fail("allocation");
-      BVH_DEV(hipMemcpyAsync(dchunks.p, ch.data(), NC * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
-      BVH_DEV(hipMemcpyAsync(dgroups.p, grp.data(), NG * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(dtasks.p, SG.tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(dchunks.p, SG.ch.data(), NC * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(dgroups.p, SG.grp.data(), NG * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
       k_stage_copy<<<NC0, 256, 0, st>>>(dchunks.p, ids3.p, backup.p, n);
-      segs.clear();
-      segs.reserve(3 * (size_t)T);
-      for (int a = 0; a < 3; ++a)
-        for (const Task &tk : tasks)
-          segs.push_back(Seg{a * n + tk.s, a * n + tk.e, 2 * lg2(tk.e - tk.s), 0});
       pt.hstop(0);
-      if (S.sort(segs)) return fail("sort");
+      if (S.sort(SG.segs)) return fail("sort");
       pt.start();
       k_sah_chunk_box<<<NC, kSahT, 0, st>>>(dchunks.p, ids3.p, tbox.p, n, cbox.p);
       k_sah_carry<<<(NG + 63) / 64, 64, 0, st>>>(dgroups.p, NG, cbox.p, cpre.p, csuf.p, dpsa.p);
@@ -1004,111 +989,25 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       BVH_DEV(hipMemcpyAsync(hcd.data(), cdivv.p, NC * 4, hipMemcpyDeviceToHost, st), "SAH sweep");
       BVH_DEV(hipStreamSynchronize(st), "SAH sweep");
       pt.stop(2);
-      // first minimum over the chunks of each (candidate, axis): (cost, divider) lexicographic
-      for (uint32_t g = 0; g < NG; ++g) {
-        float bc = __builtin_huge_valf();
-        uint32_t bd = 0xFFFFFFFFu;
-        for (uint32_t k = grp[g].first; k < grp[g].first + grp[g].count; ++k)
-          if (hcc[k] < bc || (hcc[k] == bc && hcd[k] < bd)) {
-            bc = hcc[k];
-            bd = hcd[k];
-          }
-        // cost/dvd are indexed [3 * task + axis], as the single-workgroup sweep wrote them
-        cost[g] = bc;
-        dvd[g] = bd;
-      }
+      pt.hstart();
+      SG.reduce_sah(hcc.data(), hcd.data());
     }
-    pt.hstart();
     // createNode's FIFO, candidate by candidate (triangles_raytracing.cpp:162-173)
-    next.clear();
-    for (size_t o = 0; o < open.size(); ++o) {
-      Open &N = open[o];
-      CandQueue q2;
-      bool capped = false;
-      for (size_t c = 0; c < N.queue.size(); ++c) {
-        const auto cand = N.queue[c];
-        const int ti = task_of[task_off[o] + c];
-        if (N.nd == 7) {  // the reference stops here: this candidate is never tried
-          capped = true;
-          if (ti >= 0) action[ti] = 3;
-          continue;
-        }
-        if (ti < 0) continue;  // <= 8 triangles: tryDivide returns at once
-        // tryDivide(start, end) (:119-153) from the three tryDivide(indices, start, end, axis)
-        const uint32_t start = cand.first, end = cand.second;
-        const float curSAH = static_cast<float>(end - start) / 3.0f;
-        float sah[3];
-        bool divided[3];
-        uint32_t dv3[3];
-        for (int a = 0; a < 3; ++a) {
-          const float cst = cost[(size_t)3 * ti + a];
-          divided[a] = cst < curSAH;
-          sah[a] = divided[a] ? cst : curSAH;
-          uint32_t d = dvd[(size_t)3 * ti + a] * 3;
-          if (divided[a] && (d - start) % 24 != 0) {  // align to 8 (:100-114)
-            const uint32_t d1 = (d - 1) / 24 * 24, d2 = ((d - 1) / 24 + 1) * 24;
-            const uint32_t nearest = (d - d1 <= d2 - d) ? d1 : d2, other = d1 + d2 - nearest;
-            if (start < nearest && nearest < end) d = nearest;
-            else if (start < other && other < end) d = other;
-          }
-          dv3[a] = d;
-        }
-        const float mn = std::min({curSAH, sah[0], sah[1], sah[2]});
-        int win = -1;
-        if (sah[0] == mn) win = 0;
-        else if (sah[1] == mn) win = 1;
-        else if (sah[2] == mn) win = 2;
-        action[ti] = win == 1 ? 1u : win == 2 ? 2u : 0u;
-        if (win >= 0 && divided[win]) {
-          N.div[N.nd++] = dv3[win];
-          q2.push_back({start, dv3[win]});
-          q2.push_back({dv3[win], end});
-        }
-      }
-      N.queue = (capped || N.nd == 7) ? CandQueue{} : q2;
-      if (!N.queue.empty()) {
-        next.push_back(std::move(N));
-        continue;
-      }
-      // node complete (:175-224)
-      BvhHostNode node;
-      if (N.nd == 0) {
-        if (N.end - N.start > 24) {
-          N.div[N.nd++] = ((N.start / 3 + N.end / 3) / 2) * 3;
-        } else {
-          node.leaf = true;
-          node.start = N.start;
-          node.count = N.end - N.start;
-          H[N.node] = node;
-          continue;
-        }
-      }
-      std::sort(N.div, N.div + N.nd);
-      node.nchild = (uint32_t)(N.nd + 1);
-      for (int c = 0; c <= N.nd; ++c) {
-        const uint32_t lo = c == 0 ? N.start : N.div[c - 1], hi = c == N.nd ? N.end : N.div[c];
-        node.child[c] = (int32_t)H.size();
-        H.emplace_back();
-        ranges.push_back(Task{lo / 3, hi / 3});
-        range_of.push_back({N.node, c});
-        next.push_back(Open{node.child[c], lo, hi, CandQueue::of(lo, hi), {}, 0});
-      }
-      H[N.node] = node;
-    }
+    std::string ferr;
+    if (!SG.fifo(ferr)) return hfail(ferr.c_str(), hipErrorInvalidValue);
     pt.hstop(1);
     pt.hstart();
     if (T) {
-      BVH_DEV(hipMemcpyAsync(dact.p, action.data(), T * 4, hipMemcpyHostToDevice, st), "upload");
+      BVH_DEV(hipMemcpyAsync(dact.p, SG.action.data(), T * 4, hipMemcpyHostToDevice, st), "upload");
       k_stage_apply<<<NC0, 256, 0, st>>>(dchunks.p, dact.p, ids3.p, backup.p, n);
       BVH_DEV(hipGetLastError(), "stage apply");
     }
-    if (ranges.size() > r0) {  // boxes of the children of the nodes completed in this stage
-      if (ranges.size() > max_ranges) return hfail("child range bound", hipErrorInvalidValue);
-      const uint32_t nr = (uint32_t)(ranges.size() - r0);
+    if (SG.n_ranges > r0) {  // boxes of the children of the nodes completed in this stage
+      const uint32_t nr = (uint32_t)(SG.n_ranges - r0);
       rch.clear();
       rgrp.resize(nr);
       for (uint32_t r = 0; r < nr; ++r) {
-        const Task &R = ranges[r0 + r];
+        const Task &R = SG.ranges[r0 + r];
         rgrp[r].first = (uint32_t)rch.size();
         for (uint32_t lo = R.s; lo < R.e; lo += kSahChunk)
           rch.push_back(SahChunk{r, 0u, lo, std::min<uint32_t>(R.e, lo + kSahChunk), r});
@@ -1121,43 +1020,70 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       k_sah_chunk_box<<<nrc, kSahT, 0, st>>>(drch.p, ids3.p, tbox.p, n, rcbox.p);
       k_group_fold<<<(nr + 63) / 64, 64, 0, st>>>(drgrp.p, nr, rcbox.p, boxes.p + r0);
       BVH_DEV(hipGetLastError(), "child boxes");
-      BVH_DEV(hipStreamSynchronize(st), "child boxes");  // rch / rgrp are reused by the next stage
     }
+    // the tables uploaded above are rewritten by the next stage's host code
+    BVH_DEV(hipStreamSynchronize(st), "stage end");
     pt.hstop(2);
-    open.swap(next);
+    SG.advance();
   }
   if (pt.on) {
     (void)hipStreamSynchronize(st);
     pt.acc[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
   }
   pt.start();
-  // the child boxes, and the final triangle order
-  std::vector<uint32_t> cur(n);
-  if (!ranges.empty()) {
-    std::vector<TBox> hb(ranges.size());
+  // the child boxes, and the final triangle order when the host needs it
+  const bool dev_tris = (want & kBvhTris) && (want & kBvhDeviceTris);
+  std::vector<uint32_t> cur;
+  if (SG.n_ranges) {
+    std::vector<TBox> hb(SG.n_ranges);
     BVH_DEV(hipMemcpyAsync(hb.data(), boxes.p, hb.size() * sizeof(TBox), hipMemcpyDeviceToHost, st), "child boxes");
     BVH_DEV(hipStreamSynchronize(st), "child boxes");
-    for (size_t r = 0; r < ranges.size(); ++r) {
-      BvhBox &b = H[range_of[r].first].box[range_of[r].second];
+    for (size_t r = 0; r < SG.n_ranges; ++r) {
+      BvhBox &b = SG.H[SG.range_of[r].first].box[SG.range_of[r].second];
       std::memcpy(b.mn, hb[r].mn, 12);
       std::memcpy(b.mx, hb[r].mx, 12);
     }
   }
-  BVH_DEV(hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st), "download");
-  BVH_DEV(hipStreamSynchronize(st), "download");
+  if ((want & kBvhPerm) || ((want & kBvhTris) && !dev_tris)) {
+    cur.resize(n);
+    BVH_DEV(hipMemcpyAsync(cur.data(), ids3.p, (size_t)n * 4, hipMemcpyDeviceToHost, st), "download");
+    BVH_DEV(hipStreamSynchronize(st), "download");
+  }
   pt.stop(6);
   pt.start();
-  bvh_layout(vpos4, idx, nidx, HostNodes(H.p, H.size()), cur, out, with_canon);
+  bvh_layout(vpos4, idx, nidx, HostNodes(SG.H.p, SG.n_nodes), cur, out, want, !dev_tris);
   pt.stop(3);
+  if (dev_tris) {  // the leaf triangles straight from the device-side order (bvh_layout's fill_tris)
+    pt.start();
+    const uint32_t nl = (uint32_t)(out.leaf_tab.size() / 3);
+    DBuf<uint32_t> dtab;
+    void *tp = nullptr;
+    const size_t tbytes = ((size_t)out.n_tris + 8) * sizeof(rtl::GTri);
+    BVH_DEV(hipMalloc(&tp, tbytes), "triangles");
+    out.dev_tris.p = tp;
+    out.dev_tris.bytes = tbytes;
+    out.dev_tris.release = [](void *q) { (void)hipFree(q); };
+    BVH_DEV(hipMemsetAsync((rtl::GTri *)tp + out.n_tris, 0, 8 * sizeof(rtl::GTri), st), "triangles");
+    if (nl) {
+      if (dtab.reserve(3 * (size_t)nl)) return fail("allocation");
+      BVH_DEV(hipMemcpyAsync(dtab.p, out.leaf_tab.data(), (size_t)nl * 12, hipMemcpyHostToDevice, st), "triangles");
+      k_fill_tris<<<(nl + 255) / 256, 256, 0, st>>>(dtab.p, nl, dv.p, didx.p, ids3.p, (rtl::GTri *)tp);
+      BVH_DEV(hipGetLastError(), "triangles");
+    }
+    BVH_DEV(hipStreamSynchronize(st), "triangles");
+    out.leaf_tab.clear();
+    out.leaf_tab.shrink_to_fit();
+    pt.stop(4);
+  }
   if (pt.on)
     std::fprintf(stderr,
                  "[bvh gpu] %u tris: total %.1f ms | alloc+upload+tri boxes %.1f, stages %.1f (partition rounds %.1f "
                  "(%d rounds), serial sorts %.1f (%d launches), SAH %.1f, other %.1f), boxes+download %.1f, layout "
-                 "%.1f; %d stages; host sections: stage prologue %.1f, FIFO %.1f, apply+boxes %.1f\n",
+                 "%.1f, device triangles %.1f; %d stages; host sections: stage prologue %.1f, FIFO %.1f, apply+boxes %.1f (minor faults %ld / %ld / %ld)\n",
                  n, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(),
                  pt.acc[7], pt.acc[5], pt.acc[0], pt.rounds, pt.acc[1], pt.serial_launches, pt.acc[2],
-                 pt.acc[5] - pt.acc[0] - pt.acc[1] - pt.acc[2], pt.acc[6], pt.acc[3], pt.stages, pt.host[0],
-                 pt.host[1], pt.host[2]);
+                 pt.acc[5] - pt.acc[0] - pt.acc[1] - pt.acc[2], pt.acc[6], pt.acc[3], pt.acc[4], pt.stages, pt.host[0],
+                 pt.host[1], pt.host[2], pt.faults[0], pt.faults[1], pt.faults[2]);
   return true;
 #undef BVH_DEV
 }

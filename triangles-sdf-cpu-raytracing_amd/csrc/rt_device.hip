@@ -1476,7 +1476,7 @@ constexpr int64_t kBvhDeviceMinTris = 32768;  // auto: the device builder from t
 thread_local int t_bvh_last = 0;
 
 int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, rth::BVHGpu &b,
-              bool with_canon) {
+              unsigned want) {
   std::string err;
   int ndev = 0;
   const bool dev = g_bvh_mode == RT_BVH_DEVICE ||
@@ -1484,7 +1484,7 @@ int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t n
                     hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0);
   bool fell_back = false;
   if (dev) {
-    if (rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err, with_canon)) {
+    if (rth::build_bvh8_gpu(vpos4, nverts, idx, nidx, b, err, want)) {
       t_bvh_last = 2;
       return RT_OK;
     }
@@ -1497,7 +1497,7 @@ int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t n
     fell_back = true;
     err.clear();
   }
-  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err, with_canon)) return set_err(RT_E_INVALID, err);
+  if (!rth::build_bvh8(vpos4, nverts, idx, nidx, b, err, want)) return set_err(RT_E_INVALID, err);
   t_bvh_last = fell_back ? 3 : 1;
   return RT_OK;
 }
@@ -1613,7 +1613,8 @@ int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64
                   uint32_t *canon, int64_t *nnodes, uint32_t *perm_tri, int32_t *max_depth) {
   if (!vpos4 || !idx || !nnodes || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "bad mesh");
   rth::BVHGpu b;
-  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, canon != nullptr)) return rc;
+  const unsigned want = (canon ? rth::kBvhCanon : 0u) | (perm_tri ? rth::kBvhPerm : 0u);
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, want)) return rc;
   const int64_t n = canon ? (int64_t)b.canon.size() / 52 : b.host_nodes;
   if (canon) {
     if (*nnodes < n) return set_err(RT_E_INVALID, "buffer too small");
@@ -1629,7 +1630,7 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
                          rt_scene **out) {
   if (!vpos4 || !idx || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "empty mesh");
   rth::BVHGpu b;
-  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, false)) return rc;
+  if (int rc = build_bvh(vpos4, nverts, idx, nidx, b, rth::kBvhTris | rth::kBvhDeviceTris)) return rc;
   int32_t maxd = 8;
   int rc = pick_maxd(b.max_depth, maxd);
   if (rc) return rc;
@@ -1643,8 +1644,12 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
   s->host_inner = b.host_inner;
   s->bvh_depth = b.max_depth;
   s->n_inner = (uint32_t)b.nodes.size();
+  if (b.dev_tris.p) {  // the device builder left the triangles on the device (with the zero pad)
+    s->dev_bytes += (int64_t)b.dev_tris.bytes;
+    s->d_tris = static_cast<rtl::GTri *>(b.dev_tris.take());
+  }
   if ((rc = upload(&s->d_nodes, b.nodes.data(), b.nodes.size(), s->dev_bytes)) ||
-      (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes))) {
+      (!s->d_tris && (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes)))) {
     rt_scene_destroy(s);
     return rc;
   }

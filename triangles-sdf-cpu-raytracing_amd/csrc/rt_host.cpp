@@ -476,7 +476,7 @@ struct Builder {
 }  // namespace
 
 bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                std::string &err, bool with_canon) {
+                std::string &err, unsigned want) {
   if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
   const size_t ntri = (size_t)nidx / 3;
   for (int64_t i = 0; i < nidx; ++i)
@@ -513,20 +513,16 @@ bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t
     B.create(0, 0, (size_t)nidx);
   }
 
-  bvh_layout(vpos4, idx, nidx, B.nodes, B.cur, out, with_canon);
+  bvh_layout(vpos4, idx, nidx, B.nodes, B.cur, out, want, true);
   return true;
 }
 
 void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, HostNodes H,
-                const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon) {
-  const int64_t ntri = nidx / 3;
+                const std::vector<uint32_t> &cur, BVHGpu &out, unsigned want, bool host_tris) {
+  (void)nidx;
   out.host_nodes = (int64_t)H.size();
-  out.perm_tri = cur;
-  out.perm_idx.resize((size_t)nidx);
-#pragma omp parallel for schedule(static)
-  for (int64_t t = 0; t < ntri; ++t)
-    for (int k = 0; k < 3; ++k) out.perm_idx[3 * t + k] = idx[3 * (size_t)cur[t] + k];
-  if (with_canon) {  // canonical pre-order (52 u32 per node), same as the oracle's export
+  if (want & kBvhPerm) out.perm_tri = cur;
+  if (want & kBvhCanon) {  // canonical pre-order (52 u32 per node), same as the oracle's export
     out.canon.reserve(H.size() * 52);
     std::vector<int32_t> st{0};
     while (!st.empty()) {
@@ -569,6 +565,17 @@ void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, HostNodes
     return rtl::kLeafBit | (first << 3) | (nt - 1);
   };
   auto fill_tris = [&]() {
+    out.n_tris = next_slot;
+    if (!(want & kBvhTris)) return;
+    if (!host_tris) {  // the caller fills them (the device builder)
+      out.leaf_tab.resize(3 * leaf_fill.size());
+      for (size_t l = 0; l < leaf_fill.size(); ++l) {
+        out.leaf_tab[3 * l] = leaf_fill[l].first;
+        out.leaf_tab[3 * l + 1] = leaf_fill[l].second;
+        out.leaf_tab[3 * l + 2] = leaf_cnt[l];
+      }
+      return;
+    }
     out.tris.resize(next_slot);
 #pragma omp parallel for schedule(dynamic, 256)
     for (int64_t l = 0; l < (int64_t)leaf_fill.size(); ++l) {

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "rt_layout.h"
@@ -21,21 +22,60 @@ bool load_obj(const char *path, bool scale, Mesh &out, std::string &err);
 bool load_grid(const char *path, uint32_t size[3], std::vector<float> &values, std::string &err);
 bool load_octree(const char *path, std::vector<uint8_t> &nodes36, std::string &err);
 
+// What a BVH build returns besides the inner nodes, root and depth (BVHGpu).
+enum : unsigned {
+  kBvhCanon = 1,       // BVHGpu::canon (rt_bvh_export)
+  kBvhPerm = 2,        // BVHGpu::perm_tri (rt_bvh_export)
+  kBvhTris = 4,        // the leaf triangles (BVHGpu::tris)
+  kBvhDeviceTris = 8,  // with kBvhTris: the device builder may leave them on the device (BVHGpu::dev_tris)
+  kBvhAll = kBvhCanon | kBvhPerm | kBvhTris,
+};
+// A device allocation handed from the builder to the scene (move-only).
+struct DevBuffer {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void (*release)(void *) = nullptr;
+  DevBuffer() = default;
+  DevBuffer(const DevBuffer &) = delete;
+  DevBuffer &operator=(const DevBuffer &) = delete;
+  DevBuffer(DevBuffer &&o) noexcept { swap(o); }
+  DevBuffer &operator=(DevBuffer &&o) noexcept {
+    DevBuffer t(std::move(o));
+    swap(t);
+    return *this;
+  }
+  ~DevBuffer() {
+    if (p && release) release(p);
+  }
+  void swap(DevBuffer &o) noexcept {
+    std::swap(p, o.p);
+    std::swap(bytes, o.bytes);
+    std::swap(release, o.release);
+  }
+  void *take() {  // the caller owns (and frees) it from here on
+    void *q = p;
+    p = nullptr;
+    return q;
+  }
+};
 struct BVHGpu {
   std::vector<rtl::GNode> nodes;   // inner nodes, BFS order, root = 0
   std::vector<rtl::GTri> tris;     // leaf triangles, leaves in BFS order of their parents
+  DevBuffer dev_tris;              // or these on the device (kBvhDeviceTris), followed by 8 zero triangles
+  uint32_t n_tris = 0;             // triangle slots (either form)
   uint32_t root_word = rtl::kInvalidChild;
   float root_box[6] = {0, 0, 0, 0, 0, 0};  // union of the root's child boxes (inner root)
   int32_t max_depth = 0;           // inner nodes on the deepest root->leaf path
   int64_t host_nodes = 0, host_inner = 0;
   // canonical pre-order export (52 x u32 per node), for parity with the oracle
   std::vector<uint32_t> canon;
-  std::vector<uint32_t> perm_idx;  // mesh indices after the build's permutation
   std::vector<uint32_t> perm_tri;  // original triangle id per triangle slot
+  // leaves whose triangles bvh_layout did not write (no kBvhTris on the host):
+  // (first slot, first triangle position, count) per leaf
+  std::vector<uint32_t> leaf_tab;
 };
-// with_canon: also fill BVHGpu::canon (rt_bvh_export; scene creation skips it)
 bool build_bvh8(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                std::string &err, bool with_canon = true);
+                std::string &err, unsigned want = kBvhAll);
 
 // The tree BVHBuilder::perform builds (triangles_raytracing.cpp:155-225), as
 // either builder produces it: nodes (node 0 = root; children anywhere) and the
@@ -62,14 +102,16 @@ struct HostNodes {
   size_t size() const { return n; }
   const BvhHostNode &operator[](size_t i) const { return p[i]; }
 };
-// Canonical export + GPU layout (GNode / GTri, BFS over inner nodes) of a built tree.
+// Canonical export + GPU layout (GNode / GTri, BFS over inner nodes) of a
+// built tree; `cur` (the triangle order) is read for kBvhPerm and host kBvhTris
+// only. host_tris false: the leaf table instead of BVHGpu::tris.
 void bvh_layout(const float *vpos4, const uint32_t *idx, int64_t nidx, HostNodes H,
-                const std::vector<uint32_t> &cur, BVHGpu &out, bool with_canon = true);
+                const std::vector<uint32_t> &cur, BVHGpu &out, unsigned want, bool host_tris);
 // The same tree built on the current HIP device (rt_bvhgpu.hip): libstdc++'s
 // introsort replicated with parallel Hoare partitions, SAH sweeps as device
 // scans. Identical output to build_bvh8.
 bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
-                    std::string &err, bool with_canon = true);
+                    std::string &err, unsigned want = kBvhAll);
 
 struct OctGpu {
   std::vector<rtl::OctWord> child;    // per node: {0 leaf, kOctNeverHits or childrenOffset; child masks}

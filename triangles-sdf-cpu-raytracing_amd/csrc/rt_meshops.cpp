@@ -43,7 +43,7 @@ struct KeyHash {
 bool prep_sdf_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
                    SdfMeshHost &out, std::string &err) {
   out = SdfMeshHost();
-  if (!build_bvh8(vpos4, nverts, idx, nidx, out.bvh, err)) return false;
+  if (!build_bvh8(vpos4, nverts, idx, nidx, out.bvh, err, kBvhTris)) return false;
   const size_t ntri = (size_t)nidx / 3;
   if (ntri == 0) { err = "mesh has no triangles"; return false; }
 
