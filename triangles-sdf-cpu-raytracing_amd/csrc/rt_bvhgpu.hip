@@ -184,38 +184,130 @@ __device__ void d_introsort(KI *base, uint32_t len, int depth, uint32_t *stk) {
   }
 }
 
+// set bits of m below this lane
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// std::__introsort_loop by one wave (a 64-thread block) on LDS. Each
+// std::__unguarded_partition_pivot runs as in the partition rounds: the
+// a-elements (stop the left scan) and b-elements (stop the right scan) are
+// listed by ballots, and the k-th a from the left swaps with the k-th b from
+// the right while it lies left of it -- all such pairs at once (every left
+// one lies left of every right one). The ranges of <= 16 left for the final
+// insertion sort are listed in `leaf` (first | last << 16); returns their
+// count. Heapsorted ranges (depth 0) are already sorted and not listed.
+__device__ uint32_t wave_introsort(KI *a, uint32_t len, int depth, uint16_t *Lp, uint16_t *Bp, uint32_t *stk,
+                                   uint32_t *leaf) {
+  const uint32_t lane = threadIdx.x;
+  const auto less = [](const KI &x, const KI &y) { return x.k < y.k; };
+  uint32_t f = 0, l = len, nleaf = 0;
+  int sp = 0;
+  for (;;) {
+    bool heaped = false;
+    while (l - f > 16) {
+      if (depth == 0) {
+        if (lane == 0) d_heapsort(a + f, a + l, less);
+        heaped = true;
+        break;
+      }
+      --depth;
+      if (lane == 0) d_median_to_first(a + f, a + f + 1, a + f + (l - f) / 2, a + l - 1, less);
+      __syncthreads();
+      const float pk = a[f].k;
+      uint32_t na = 0, nb = 0;
+      for (uint32_t base = f; base < l; base += 64) {
+        const uint32_t p = base + lane;
+        const bool v = p < l;
+        const float k = v ? a[p].k : 0.0f;
+        const bool fa = v && p != f && !(k < pk), fb = v && (p == f || !(pk < k));
+        const uint64_t ma = __ballot(fa), mb = __ballot(fb);
+        if (fa) Lp[na + lane_prefix(ma)] = (uint16_t)p;
+        if (fb) Bp[nb + lane_prefix(mb)] = (uint16_t)p;
+        na += (uint32_t)__popcll(ma);
+        nb += (uint32_t)__popcll(mb);
+      }
+      __syncthreads();
+      uint32_t sw = 0;  // pairs that swap: L_k < R_k, monotone in k
+      for (uint32_t kb = 0; kb < na; kb += 64) {
+        const uint32_t k = kb + lane + 1;
+        sw += (uint32_t)__popcll(__ballot(k <= na && k <= nb && Lp[k - 1] < Bp[nb - k]));
+      }
+      for (uint32_t kb = 0; kb < sw; kb += 64) {
+        const uint32_t k = kb + lane + 1;
+        if (k <= sw) {
+          const uint32_t x = Lp[k - 1], y = Bp[nb - k];
+          const KI t = a[x];
+          a[x] = a[y];
+          a[y] = t;
+        }
+      }
+      // where the left scan stops after the last swap (the median of three
+      // guarantees an a-element)
+      const uint32_t cut = sw == 0 ? Lp[0] : (sw < na ? min((uint32_t)Lp[sw], (uint32_t)Bp[nb - sw])
+                                                       : (uint32_t)Bp[nb - sw]);
+      __syncthreads();
+      if (lane == 0) {
+        stk[2 * sp] = (cut << 16) | l;
+        stk[2 * sp + 1] = (uint32_t)depth;
+      }
+      ++sp;
+      l = cut;
+    }
+    if (!heaped && l - f > 1) {
+      if (lane == 0) leaf[nleaf] = f | (l << 16);
+      ++nleaf;
+    }
+    __syncthreads();
+    if (sp == 0) break;
+    --sp;
+    const uint32_t w = stk[2 * sp];
+    depth = (int)stk[2 * sp + 1];
+    f = w >> 16;
+    l = w & 0xFFFFu;
+  }
+  return nleaf;
+}
+
 // one wave per short segment (<= kSerialMax): (key, id) pairs staged in LDS,
-// the rest of the introsort and the final insertion sort by lane 0
-__global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t *ids, const float *K3, uint32_t n) {
+// the introsort loop by the wave, then the final insertion sort as one
+// insertion sort per leaf range, a lane each (it never moves an element
+// across a partition boundary, so the order is std::sort's)
+__global__ __launch_bounds__(64) void k_serial(const Seg *segs, uint32_t *ids, float *kv, const float *K3,
+                                               uint32_t n) {
   __shared__ KI a[kSerialMax];
-  __shared__ uint32_t stk[2 * 64];
+  __shared__ uint16_t Lp[kSerialMax], Bp[kSerialMax];
+  __shared__ uint32_t stk[2 * 64], leaf[kSerialMax];
   const Seg s = segs[blockIdx.x];
-  const float *K = K3 + (size_t)(s.first / n) * n;
   const uint32_t len = s.last - s.first;
   if (len > kSerialMax) {  // a long segment whose depth ran out (k_prep): heapsort in place
+    const float *K = K3 + (size_t)(s.first / n) * n;
     if (threadIdx.x == 0)
       d_heapsort(ids + s.first, ids + s.last, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < len; i += 64) kv[s.first + i] = K[ids[s.first + i]];
     return;  // sorted: the final insertion sort leaves it unchanged
   }
+  for (uint32_t i = threadIdx.x; i < len; i += 64) a[i] = KI{kv[s.first + i], ids[s.first + i]};
+  __syncthreads();
+  const uint32_t nl = wave_introsort(a, len, s.depth, Lp, Bp, stk, leaf);
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nl; j += 64) d_insertion(a + (leaf[j] & 0xFFFFu), a + (leaf[j] >> 16));
+  __syncthreads();
   for (uint32_t i = threadIdx.x; i < len; i += 64) {
-    const uint32_t id = ids[s.first + i];
-    a[i] = KI{K[id], id};
+    ids[s.first + i] = a[i].id;
+    kv[s.first + i] = a[i].k;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    d_introsort(a, len, s.depth, stk);
-    d_insertion(a, a + len);
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < len; i += 64) ids[s.first + i] = a[i].id;
 }
 
 // ---- one round of parallel introsort partitions ----------------------------
 // A round is six launches that read the round's segment count m and element
-// count E from device memory (RoundCtl), so the host enqueues several rounds
-// back to back with upper bounds for the grids and synchronises once per batch
-// (a round whose m is 0 exits at once). Element space of a round: the active
-// segments back to back (virtual index v; segment i covers [offs[i], offs[i+1])).
+// count E from device memory (the ctl words), so the host enqueues several
+// rounds back to back with upper bounds for the grids and synchronises once
+// per batch (a round whose m is 0 exits at once). Element space of a round:
+// the active segments back to back (virtual index v; segment i covers
+// [offs[i], offs[i+1])). Keys travel with the ids (kv[p] = K[ids[p]], swapped
+// together), so a round reads them coalesced instead of gathering K[id].
 constexpr int kRoundT = 256, kRoundI = 8, kRoundTile = kRoundT * kRoundI;
 constexpr int kMaxRounds = 64;  // > the introsort depth limit 2 lg2(3n) + 1: a sort never needs more
 // ctl words: [0] serial-list count, [1..3] unused, then (m, E) of round r at [4 + 2 r]
@@ -261,23 +353,32 @@ struct Round {
 
 // per segment: median to the front, pivot key, size (0: depth exhausted, the
 // segment goes to the serial list, whose introsort loop heapsorts it)
-__global__ __launch_bounds__(kRoundT) void k_prep(Round R, uint32_t *ids, const float *K3, uint32_t n, float *kp,
-                                                  uint32_t *size, uint32_t *sw, Seg *serial) {
+__global__ __launch_bounds__(kRoundT) void k_prep(Round R, uint32_t *ids, float *kv, float *kp, uint32_t *size,
+                                                  Seg *serial) {
   const uint32_t m = R.m(), i = blockIdx.x * kRoundT + threadIdx.x;
-  if (i < m) {
-    const Seg s = R.cur[i];
-    sw[i] = 0;
-    if (s.depth == 0) {
-      serial[atomicAdd(&R.ctl[0], 1u)] = s;
-      size[i] = 0;
-    } else {
-      const float *K = K3 + (size_t)(s.first / n) * n;
-      uint32_t *f = ids + s.first, *l = ids + s.last;
-      d_median_to_first(f, f + 1, f + (l - f) / 2, l - 1, [K](uint32_t x, uint32_t y) { return K[x] < K[y]; });
-      kp[i] = K[*f];
-      size[i] = s.last - s.first;
-    }
+  if (i >= m) return;
+  const Seg s = R.cur[i];
+  if (s.depth == 0) {
+    serial[atomicAdd(&R.ctl[0], 1u)] = s;
+    size[i] = 0;
+    return;
   }
+  // std::__move_median_to_first on (id, key) pairs
+  const uint32_t f = s.first, l = s.last, mid = f + (l - f) / 2;
+  const uint32_t pos[3] = {f + 1, mid, l - 1};
+  const float a = kv[pos[0]], b = kv[pos[1]], c = kv[pos[2]];
+  int w;  // which of the three moves to the front
+  if (a < b) w = (b < c) ? 1 : (a < c) ? 2 : 0;
+  else w = (a < c) ? 0 : (b < c) ? 2 : 1;
+  const uint32_t q = pos[w];
+  const uint32_t t = ids[f];
+  const float tk = kv[f], pk = kv[q];
+  ids[f] = ids[q];
+  kv[f] = pk;
+  ids[q] = t;
+  kv[q] = tk;
+  kp[i] = pk;
+  size[i] = l - f;
 }
 // one block: the segment sizes into offs[0..m] (exclusive, offs[m] = E)
 __global__ __launch_bounds__(kRoundT) void k_scan_sizes(Round R, const uint32_t *size, uint32_t *offs) {
@@ -298,77 +399,79 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t *offs, uint32_t m, uin
 // Prefix counts of the two flag kinds over the round's elements:
 // a = stops the left scan of the partition (!(key < pivot), the pivot itself
 // excluded), b = stops the right scan (!(pivot < key), the pivot included).
-// Per tile of kRoundTile elements the in-tile inclusive counts (Aloc / Bloc),
-// the tile totals (exclusive-scanned over the tiles by k_scan_tiles), and
-// per segment the in-tile count before its first element (startA / startB)
-// and through its last (endA / endB). Global inclusive count at v:
-// tileA[v / tile] + Aloc[v].
+// Per tile of kRoundTile elements the in-tile inclusive counts (AB: a in bits
+// 0-15, b in 16-31), the tile totals (exclusive-scanned over the tiles by
+// k_scan_tiles), and per segment the in-tile count before its first element
+// (startA / startB) and through its last (endA / endB).
 struct Prefix {
-  uint32_t *Aloc, *Bloc, *tileA, *tileB, *startA, *startB, *endA, *endB;
-  __device__ uint32_t a_at(uint32_t v) const { return tileA[v / kRoundTile] + Aloc[v]; }
-  __device__ uint32_t b_at(uint32_t v) const { return tileB[v / kRoundTile] + Bloc[v]; }
+  uint32_t *AB, *tileA, *tileB, *startA, *startB, *endA, *endB;
+  __device__ uint32_t a_at(uint32_t v) const { return tileA[v / kRoundTile] + (AB[v] & 0xFFFFu); }
+  __device__ uint32_t b_at(uint32_t v) const { return tileB[v / kRoundTile] + (AB[v] >> 16); }
   // a / b elements before segment i (o = its first element) and through it (oe = one past its last)
   __device__ uint32_t a_before(uint32_t i, uint32_t o) const { return tileA[o / kRoundTile] + startA[i]; }
   __device__ uint32_t b_before(uint32_t i, uint32_t o) const { return tileB[o / kRoundTile] + startB[i]; }
-  __device__ uint32_t a_through(uint32_t i, uint32_t oe) const { return tileA[(oe - 1) / kRoundTile] + endA[i]; }
   __device__ uint32_t b_through(uint32_t i, uint32_t oe) const { return tileB[(oe - 1) / kRoundTile] + endB[i]; }
+  __device__ uint32_t a_through(uint32_t i, uint32_t oe) const { return tileA[(oe - 1) / kRoundTile] + endA[i]; }
 };
 
-__global__ __launch_bounds__(kRoundT) void k_flags(Round R, const uint32_t *offs, const uint32_t *ids,
-                                                   const float *K3, uint32_t n, const float *kp, uint8_t *fl,
-                                                   uint32_t *segv, Prefix P) {
-  __shared__ uint32_t sm[kRoundT];
+// A tile is 4 waves x 512 elements; a wave walks its 512 in 8 coalesced
+// chunks of 64 (lane = element), counting the flags with ballots.
+__global__ __launch_bounds__(kRoundT) void k_flags(Round R, const uint32_t *offs, const float *kv, const float *kp,
+                                                   uint8_t *fl, uint32_t *segv, Prefix P) {
+  constexpr uint32_t kWaveSpan = kRoundTile / (kRoundT / 64);
+  __shared__ uint32_t wsum[kRoundT / 64];
   const uint32_t m = R.m(), E = offs[m];
-  if (blockIdx.x * kRoundTile >= E) return;
-  const uint32_t b0 = blockIdx.x * kRoundTile + threadIdx.x * kRoundI;
-  uint32_t f[kRoundI], cnt = 0;  // packed counts: a in bits 0-15, b in 16-31 (<= 2048 each per tile)
-  uint32_t i = b0 < E ? seg_of(offs, m, b0) : 0;
+  const uint32_t t0 = blockIdx.x * kRoundTile;
+  if (t0 >= E) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u, wb = t0 + w * kWaveSpan;
+  uint32_t i = wb < E ? seg_of(offs, m, wb) : 0;  // segment of this chunk's first element (wave-uniform)
+  uint32_t inc[kRoundI], seg[kRoundI], run = 0;   // in-wave inclusive packed counts (a | b << 16)
+  uint8_t fk[kRoundI];
 #pragma unroll
-  for (int k = 0; k < kRoundI; ++k) {
-    const uint32_t v = b0 + k;
-    f[k] = 0;
+  for (int c = 0; c < kRoundI; ++c) {
+    const uint32_t v = wb + c * 64 + lane;
+    bool fa = false, fb = false;
+    uint32_t il = i;
     if (v < E) {
-      while (offs[i + 1] <= v) ++i;  // zero-size segments (serial) are skipped
-      const Seg s = R.cur[i];
-      const uint32_t p = s.first + (v - offs[i]);
-      const float key = K3[(size_t)(s.first / n) * n + ids[p]], pk = kp[i];
-      f[k] = ((p != s.first && !(key < pk)) ? 1u : 0u) | ((p == s.first || !(pk < key)) ? 0x10000u : 0u);
-      segv[v] = i;
-      fl[v] = (uint8_t)((f[k] & 1u) | (f[k] >> 15));
+      while (offs[il + 1] <= v) ++il;  // zero-size segments (serial) are skipped
+      const uint32_t o = offs[il];
+      const float key = kv[R.cur[il].first + (v - o)], pk = kp[il];
+      fa = v != o && !(key < pk);
+      fb = v == o || !(pk < key);
+      segv[v] = il;
+      fl[v] = (uint8_t)((fa ? 1u : 0u) | (fb ? 2u : 0u));
     }
-    cnt += f[k];
+    const uint64_t ma = __ballot(fa), mb = __ballot(fb);
+    inc[c] = run + ((lane_prefix(ma) + (fa ? 1u : 0u)) | ((lane_prefix(mb) + (fb ? 1u : 0u)) << 16));
+    run += (uint32_t)__popcll(ma) | ((uint32_t)__popcll(mb) << 16);
+    fk[c] = (uint8_t)((fa ? 1u : 0u) | (fb ? 2u : 0u));
+    seg[c] = il;
+    i = (uint32_t)__shfl((int)il, 63);
   }
-  sm[threadIdx.x] = cnt;
+  if (lane == 0) wsum[w] = run;
   __syncthreads();
-  for (int o = 1; o < kRoundT; o <<= 1) {
-    const uint32_t x = threadIdx.x >= (uint32_t)o ? sm[threadIdx.x - o] : 0u;
-    __syncthreads();
-    sm[threadIdx.x] += x;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? sm[threadIdx.x - 1] : 0u;
-  i = b0 < E ? seg_of(offs, m, b0) : 0;
+  uint32_t woff = 0;
+  for (uint32_t k = 0; k < w; ++k) woff += wsum[k];
 #pragma unroll
-  for (int k = 0; k < kRoundI; ++k) {
-    const uint32_t v = b0 + k;
-    if (v < E) {
-      while (offs[i + 1] <= v) ++i;
-      if (v == offs[i]) {
-        P.startA[i] = run & 0xFFFFu;
-        P.startB[i] = run >> 16;
-      }
-      run += f[k];
-      P.Aloc[v] = run & 0xFFFFu;
-      P.Bloc[v] = run >> 16;
-      if (v + 1 == offs[i + 1]) {
-        P.endA[i] = run & 0xFFFFu;
-        P.endB[i] = run >> 16;
-      }
+  for (int c = 0; c < kRoundI; ++c) {
+    const uint32_t v = wb + c * 64 + lane;
+    if (v >= E) continue;
+    const uint32_t in = woff + inc[c], il = seg[c];
+    P.AB[v] = in;
+    if (v == offs[il]) {
+      const uint32_t ex = in - ((fk[c] & 1u) | ((uint32_t)(fk[c] >> 1) << 16));
+      P.startA[il] = ex & 0xFFFFu;
+      P.startB[il] = ex >> 16;
+    }
+    if (v + 1 == offs[il + 1]) {
+      P.endA[il] = in & 0xFFFFu;
+      P.endB[il] = in >> 16;
     }
   }
-  if (threadIdx.x == kRoundT - 1) {
-    P.tileA[blockIdx.x] = sm[kRoundT - 1] & 0xFFFFu;
-    P.tileB[blockIdx.x] = sm[kRoundT - 1] >> 16;
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    P.tileA[blockIdx.x] = tot & 0xFFFFu;
+    P.tileB[blockIdx.x] = tot >> 16;
   }
 }
 // one block: the tile totals into exclusive prefixes
@@ -379,52 +482,68 @@ __global__ __launch_bounds__(kRoundT) void k_scan_tiles(Round R, const uint32_t 
   block_excl_scan(P.tileB, P.tileB, nt, sm);
 }
 
-// ranks of the a-elements from the left and the b-elements from the right,
-// scattered into per-segment position lists L, R (v-space, offs[i] + rank - 1),
-// and the number of swaps: the a-element of rank k swaps with the b-element of
-// rank k from the right while it lies left of it, i.e. while at least k
-// b-elements lie strictly right of it -- monotone in k, so the swap count is
-// the number of a-elements for which it holds (summed per wave)
+// Element blocks: ranks of the a-elements from the left and the b-elements
+// from the right, scattered into per-segment position lists L, R (v-space,
+// offs[i] + rank - 1). Segment blocks (after the element blocks, one wave per
+// segment): the swap count s. The a-element of rank k swaps with the
+// b-element of rank k from the right while it lies left of it, i.e. while at
+// least k b-elements lie strictly right of it: B_end - B(v) >= A(v) - A_before,
+// i.e. A(v) + B(v) <= B_end + A_before. A + B never decreases along the
+// segment, so the positions where that holds are a prefix [o, v*], and
+// s = A(v*) - A_before (0 when even o fails); a 64-way search finds v*.
 __global__ __launch_bounds__(kRoundT) void k_ranks(Round R, const uint32_t *offs, const uint8_t *fl,
                                                    const uint32_t *segv, Prefix P, uint32_t *Lpos, uint32_t *Rpos,
-                                                   uint32_t *sw) {
+                                                   uint32_t *sw, uint32_t eblocks) {
   const uint32_t m = R.m(), E = offs[m];
-  const uint32_t v = blockIdx.x * kRoundT + threadIdx.x;
-  const bool live = v < E;
-  uint32_t i = 0;
-  bool swaps = false;
-  if (live) {
-    i = segv[v];
-    const uint32_t o = offs[i], oe = offs[i + 1], p = R.cur[i].first + (v - o);
+  if (blockIdx.x < eblocks) {
+    const uint32_t v = blockIdx.x * kRoundT + threadIdx.x;
+    if (v >= E) return;
     const uint8_t f = fl[v];
-    if (f & 1u) {
-      const uint32_t rank = P.a_at(v) - P.a_before(i, o);
-      Lpos[o + rank - 1] = p;
-      swaps = P.b_through(i, oe) - P.b_at(v) >= rank;  // b-elements strictly right of p
-    }
+    if (!f) return;
+    const uint32_t i = segv[v], o = offs[i], p = R.cur[i].first + (v - o);
+    if (f & 1u) Lpos[o + (P.a_at(v) - P.a_before(i, o)) - 1] = p;
     if (f & 2u) {
-      const uint32_t btot = P.b_through(i, oe) - P.b_before(i, o), rank = P.b_at(v) - P.b_before(i, o);
+      const uint32_t bb = P.b_before(i, o);
+      const uint32_t btot = P.b_through(i, offs[i + 1]) - bb, rank = P.b_at(v) - bb;
       Rpos[o + (btot - rank)] = p;
     }
+    return;
   }
-  const uint64_t act = __ballot(live);
-  if (act == 0) return;
-  const uint32_t i0 = (uint32_t)__shfl(i, __ffsll((unsigned long long)act) - 1);
-  if (__ballot(live && i != i0) == 0) {  // one segment in this wave: one atomic
-    const uint32_t c = (uint32_t)__popcll(__ballot(swaps));
-    if (c && (int)(threadIdx.x & 63u) == __ffsll((unsigned long long)act) - 1) atomicAdd(&sw[i0], c);
-  } else if (swaps) {
-    atomicAdd(&sw[i], 1u);
+  const uint32_t i = (blockIdx.x - eblocks) * (kRoundT / 64) + threadIdx.x / 64, lane = threadIdx.x & 63u;
+  if (i >= m) return;
+  const uint32_t o = offs[i], oe = offs[i + 1];
+  if (o == oe) return;  // depth exhausted: serial
+  const uint32_t ab = P.a_before(i, o), C = P.b_through(i, oe) + ab;
+  // largest v in [o, oe) with A(v) + B(v) <= C; the candidates are [lo, hi]
+  uint32_t lo = o, hi = oe - 1;
+  if (P.a_at(lo) + P.b_at(lo) > C) {
+    if (lane == 0) sw[i] = 0;
+    return;
   }
+  while (hi > lo) {  // invariant: F(lo) <= C
+    const uint32_t len = hi - lo, step = (len + 63) / 64;
+    const uint32_t pr = min(hi, lo + (lane + 1) * step);
+    const bool ok = P.a_at(pr) + P.b_at(pr) <= C;
+    const uint64_t bm = __ballot(ok);  // a prefix of the lanes (F is monotone; clamped probes repeat hi)
+    const int j = bm ? 63 - __clzll((unsigned long long)bm) : -1;  // last lane that holds
+    if (j < 0) {
+      hi = min(hi, lo + step) - 1;  // the answer lies in [lo, lo + step - 1]
+    } else {
+      const uint32_t at = min(hi, lo + (uint32_t)(j + 1) * step);
+      lo = at;
+      hi = (j == 63 || at == hi) ? hi : min(hi, at + step - 1);
+    }
+  }
+  if (lane == 0) sw[i] = P.a_at(lo) - ab;
 }
 
-// the swaps (one thread per pair: its a-element) and, per segment, the cut
-// (where the left scan stops after the last swap) and the two parts: longer
-// than kSerialMax -> the next round, else the serial list
+// the swaps (one thread per pair: its a-element, ids and keys together) and,
+// per segment, the cut (where the left scan stops after the last swap) and
+// the two parts: longer than kSerialMax -> the next round, else the serial list
 __global__ __launch_bounds__(kRoundT) void k_swap_split(Round R, const uint32_t *offs, const uint32_t *size,
                                                         const uint8_t *fl, const uint32_t *segv, Prefix P,
                                                         const uint32_t *Lpos, const uint32_t *Rpos,
-                                                        const uint32_t *sw, uint32_t *ids, Seg *serial) {
+                                                        const uint32_t *sw, uint32_t *ids, float *kv, Seg *serial) {
   const uint32_t m = R.m(), E = offs[m];
   const uint32_t t = blockIdx.x * kRoundT + threadIdx.x;
   if (t < E && (fl[t] & 1u)) {
@@ -433,8 +552,11 @@ __global__ __launch_bounds__(kRoundT) void k_swap_split(Round R, const uint32_t 
     if (rank <= sw[i]) {
       const uint32_t p = R.cur[i].first + (t - o), q = Rpos[o + rank - 1];
       const uint32_t x = ids[p];
+      const float xk = kv[p];
       ids[p] = ids[q];
+      kv[p] = kv[q];
       ids[q] = x;
+      kv[q] = xk;
     }
   }
   if (t >= m || size[t] == 0) return;
@@ -637,23 +759,30 @@ __global__ __launch_bounds__(kSahT) void k_sah_chunk_cost(const SahChunk *chunks
 // scratch; one workgroup per kSahChunk-triangle chunk of a candidate (the axis-0
 // chunks of the SAH table), so a stage of a few huge candidates is not left to
 // a few workgroups
-__global__ void k_stage_copy(const SahChunk *chunks, uint32_t *ids3, uint32_t *backup, uint32_t n) {
+__global__ void k_stage_copy(const SahChunk *chunks, uint32_t *ids3, float *kv3, const float *K3, uint32_t *backup,
+                             uint32_t n) {
   const SahChunk c = chunks[blockIdx.x];
   for (uint32_t t = c.lo + threadIdx.x; t < c.hi; t += blockDim.x) {
     const uint32_t v = ids3[t];
     backup[t] = v;
     ids3[n + t] = v;
     ids3[2 * n + t] = v;
+    kv3[n + t] = K3[n + v];
+    kv3[2 * n + t] = K3[2 * n + v];
   }
 }
 // stage end: 1 = take the Y order, 2 = the Z order, 3 = restore (never evaluated by the reference)
-__global__ void k_stage_apply(const SahChunk *chunks, const uint32_t *action, uint32_t *ids3, const uint32_t *backup,
-                              uint32_t n) {
+__global__ void k_stage_apply(const SahChunk *chunks, const uint32_t *action, uint32_t *ids3, float *kv3,
+                              const float *K3, const uint32_t *backup, uint32_t n) {
   const SahChunk c = chunks[blockIdx.x];
   const uint32_t a = action[c.task];
   if (a == 0) return;
   const uint32_t *src = a == 1 ? ids3 + n : a == 2 ? ids3 + 2 * n : backup;
-  for (uint32_t t = c.lo + threadIdx.x; t < c.hi; t += blockDim.x) ids3[t] = src[t];
+  for (uint32_t t = c.lo + threadIdx.x; t < c.hi; t += blockDim.x) {
+    const uint32_t v = src[t];
+    ids3[t] = v;
+    kv3[t] = K3[v];
+  }
 }
 // child boxes (calc_bbox, :199): the ordered fold of a range's chunk unions
 // (k_sah_chunk_box on its chunks), earlier chunk on the left
@@ -667,7 +796,7 @@ __global__ void k_group_fold(const SahGroup *groups, uint32_t ng, const TBox *cb
 }
 
 // per-triangle box (calc_bbox of the /w-divided vertices, raytracing.hpp:51-60) and keys
-__global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TBox *tbox, float *K3) {
+__global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TBox *tbox, float *K3, float *kv3) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   TBox b = tb_empty();
@@ -679,6 +808,7 @@ __global__ void k_tribox(const float4 *vpos, const uint32_t *idx, uint32_t n, TB
   }
   tbox[t] = b;
   K3[t] = b.mx[0];
+  kv3[t] = b.mx[0];  // the X order starts as the identity
   K3[n + t] = b.mx[1];
   K3[2 * n + t] = b.mx[2];
 }
@@ -779,9 +909,10 @@ inline int lg2(uint64_t n) { return 63 - __builtin_clzll(n); }
 struct Sorter {
   uint32_t n = 0;  // triangles (one axis block of the 3n space)
   uint32_t *ids = nullptr;
+  float *kv = nullptr;  // kv[p] = K3[block of p][ids[p]], kept in step with ids
   const float *K3 = nullptr;
   DBuf<Seg> segA, segB, serial;
-  DBuf<uint32_t> size, offs, sw, Aloc, Bloc, tiles, bnd, segv, Lpos, Rpos, ctl;
+  DBuf<uint32_t> size, offs, sw, AB, tiles, bnd, segv, Lpos, Rpos, ctl;
   DBuf<uint8_t> fl;
   DBuf<float> kp;
   size_t segcap = 0, tilecap = 0;
@@ -789,9 +920,10 @@ struct Sorter {
   PhaseTimer own_pt;             // per build: concurrent builds share no state
   PhaseTimer *pt = &own_pt;
 
-  int init(uint32_t ntri, uint32_t *ids3, const float *keys3) {
+  int init(uint32_t ntri, uint32_t *ids3, float *kv3, const float *keys3) {
     n = ntri;
     ids = ids3;
+    kv = kv3;
     K3 = keys3;
     const size_t N = 3 * (size_t)n, sercap = N / 2 + 4096;
     segcap = N / (kSerialMax + 1) + 16;
@@ -799,7 +931,7 @@ struct Sorter {
     int rc;
     if ((rc = segA.reserve(segcap)) || (rc = segB.reserve(segcap)) || (rc = serial.reserve(sercap)) ||
         (rc = size.reserve(segcap + 1)) || (rc = offs.reserve(segcap + 1)) || (rc = sw.reserve(segcap)) ||
-        (rc = kp.reserve(segcap)) || (rc = Aloc.reserve(N)) || (rc = Bloc.reserve(N)) || (rc = fl.reserve(N)) ||
+        (rc = kp.reserve(segcap)) || (rc = AB.reserve(N)) || (rc = fl.reserve(N)) ||
         (rc = tiles.reserve(2 * tilecap)) || (rc = bnd.reserve(4 * segcap)) || (rc = segv.reserve(N)) ||
         (rc = Lpos.reserve(N)) || (rc = Rpos.reserve(N)) || (rc = ctl.reserve(kCtlWords)))
       return rc;
@@ -825,8 +957,7 @@ struct Sorter {
     if (!ser.empty()) HIP_TRY(hipMemcpyAsync(serial.p, ser.data(), ser.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
     if (m) HIP_TRY(hipMemcpyAsync(segA.p, act.data(), m * sizeof(Seg), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctl.p, hc, sizeof(hc), hipMemcpyHostToDevice, st));
-    const Prefix P{Aloc.p, Bloc.p, tiles.p, tiles.p + tilecap, bnd.p, bnd.p + segcap, bnd.p + 2 * segcap,
-                   bnd.p + 3 * segcap};
+    const Prefix P{AB.p, tiles.p, tiles.p + tilecap, bnd.p, bnd.p + segcap, bnd.p + 2 * segcap, bnd.p + 3 * segcap};
     pt->start();
     // rounds are enqueued in batches, with grid bounds: E never grows, m at
     // most doubles and each active segment holds more than kSerialMax elements;
@@ -839,14 +970,15 @@ struct Sorter {
         ++pt->rounds;
         const Round R{(r & 1) ? segB.p : segA.p, (r & 1) ? segA.p : segB.p, ctl.p, r};
         const uint32_t gm = (mb + kRoundT - 1) / kRoundT, gt = (Eb + kRoundTile - 1) / kRoundTile,
-                       ge = (std::max(Eb, mb) + kRoundT - 1) / kRoundT;
-        k_prep<<<gm, kRoundT, 0, st>>>(R, ids, K3, n, kp.p, size.p, sw.p, serial.p);
+                       ge = (std::max(Eb, mb) + kRoundT - 1) / kRoundT, eb = (Eb + kRoundT - 1) / kRoundT,
+                       gs = (mb + kRoundT / 64 - 1) / (kRoundT / 64);
+        k_prep<<<std::max(gm, 1u), kRoundT, 0, st>>>(R, ids, kv, kp.p, size.p, serial.p);
         k_scan_sizes<<<1, kRoundT, 0, st>>>(R, size.p, offs.p);
-        k_flags<<<gt, kRoundT, 0, st>>>(R, offs.p, ids, K3, n, kp.p, fl.p, segv.p, P);
+        k_flags<<<std::max(gt, 1u), kRoundT, 0, st>>>(R, offs.p, kv, kp.p, fl.p, segv.p, P);
         k_scan_tiles<<<1, kRoundT, 0, st>>>(R, offs.p, P);
-        k_ranks<<<ge, kRoundT, 0, st>>>(R, offs.p, fl.p, segv.p, P, Lpos.p, Rpos.p, sw.p);
-        k_swap_split<<<ge, kRoundT, 0, st>>>(R, offs.p, size.p, fl.p, segv.p, P, Lpos.p, Rpos.p, sw.p, ids,
-                                             serial.p);
+        k_ranks<<<eb + gs, kRoundT, 0, st>>>(R, offs.p, fl.p, segv.p, P, Lpos.p, Rpos.p, sw.p, eb);
+        k_swap_split<<<std::max(ge, 1u), kRoundT, 0, st>>>(R, offs.p, size.p, fl.p, segv.p, P, Lpos.p, Rpos.p,
+                                                           sw.p, ids, kv, serial.p);
         HIP_TRY(hipGetLastError());
         mb = std::min<uint64_t>(2ull * mb, Eb / (kSerialMax + 1));
       }
@@ -863,7 +995,7 @@ struct Sorter {
     const uint32_t nser = hc[0];
     pt->stop(0);
     pt->start();
-    if (nser) k_serial<<<nser, 64, 0, st>>>(serial.p, ids, K3, n);
+    if (nser) k_serial<<<nser, 64, 0, st>>>(serial.p, ids, kv, K3, n);
     ++pt->serial_launches;
     HIP_TRY(hipGetLastError());
     pt->stop(1);
@@ -910,7 +1042,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   pt.start();
   DBuf<float4> dv;
   DBuf<uint32_t> didx, ids3, backup, dact;
-  DBuf<float> K3;
+  DBuf<float> K3, KV3;
   DBuf<TBox> tbox, boxes, cbox, cpre, csuf;
   DBuf<Task> dtasks;
   DBuf<SahChunk> dchunks, drch;
@@ -923,11 +1055,9 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   DBuf<uint32_t> cdivv;
   Sorter S;
   if (dv.reserve((size_t)nverts) || didx.reserve((size_t)nidx) || ids3.reserve(3 * (size_t)n) ||
-      backup.reserve(n) || K3.reserve(3 * (size_t)n) || tbox.reserve(n) ||
-      S.init(n, nullptr, nullptr))
+      backup.reserve(n) || K3.reserve(3 * (size_t)n) || KV3.reserve(3 * (size_t)n) || tbox.reserve(n) ||
+      S.init(n, ids3.p, KV3.p, K3.p))
     return fail("allocation");
-  S.ids = ids3.p;
-  S.K3 = K3.p;
   S.pt = &pt;
   hipStream_t st = nullptr;
   BVH_DEV(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
@@ -942,7 +1072,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   BVH_DEV(hipMemcpyAsync(dv.p, vpos4, (size_t)nverts * 16, hipMemcpyHostToDevice, st), "upload");
   BVH_DEV(hipMemcpyAsync(didx.p, idx, (size_t)nidx * 4, hipMemcpyHostToDevice, st), "upload");
   BVH_DEV(hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st), "upload");
-  k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p);
+  k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p, KV3.p);
   BVH_DEV(hipGetLastError(), "triangle boxes");
   pt.stop(7);  // allocation, upload, triangle boxes
 
@@ -974,7 +1104,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       BVH_DEV(hipMemcpyAsync(dtasks.p, SG.tasks.data(), T * sizeof(Task), hipMemcpyHostToDevice, st), "upload");
       BVH_DEV(hipMemcpyAsync(dchunks.p, SG.ch.data(), NC * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
       BVH_DEV(hipMemcpyAsync(dgroups.p, SG.grp.data(), NG * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
-      k_stage_copy<<<NC0, 256, 0, st>>>(dchunks.p, ids3.p, backup.p, n);
+      k_stage_copy<<<NC0, 256, 0, st>>>(dchunks.p, ids3.p, KV3.p, K3.p, backup.p, n);
       pt.hstop(0);
       if (S.sort(SG.segs)) return fail("sort");
       pt.start();
@@ -999,7 +1129,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     pt.hstart();
     if (T) {
       BVH_DEV(hipMemcpyAsync(dact.p, SG.action.data(), T * 4, hipMemcpyHostToDevice, st), "upload");
-      k_stage_apply<<<NC0, 256, 0, st>>>(dchunks.p, dact.p, ids3.p, backup.p, n);
+      k_stage_apply<<<NC0, 256, 0, st>>>(dchunks.p, dact.p, ids3.p, KV3.p, K3.p, backup.p, n);
       BVH_DEV(hipGetLastError(), "stage apply");
     }
     if (SG.n_ranges > r0) {  // boxes of the children of the nodes completed in this stage
@@ -1112,27 +1242,34 @@ int rtx_sort_check(const float *keys, int64_t n, int32_t depth, uint32_t *ids_ou
   rth::host_introsort(host.data(), nn, keys, depth);
   // the sort works on a 3n space; the test uses axis block 0 only
   DBuf<uint32_t> ids3;
-  DBuf<float> K3;
+  DBuf<float> K3, KV3;
   Sorter S;
   if (int rc = ids3.reserve(3 * (size_t)nn)) return rc;
   if (int rc = K3.reserve(3 * (size_t)nn)) return rc;
-  if (int rc = S.init(nn, ids3.p, K3.p)) return rc;
+  if (int rc = KV3.reserve(3 * (size_t)nn)) return rc;
+  if (int rc = S.init(nn, ids3.p, KV3.p, K3.p)) return rc;
   HIP_TRY(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
   std::vector<uint32_t> iota(nn);
   for (uint32_t i = 0; i < nn; ++i) iota[i] = i;
   int rc = RT_OK;
   if (hipMemcpy(ids3.p, iota.data(), (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(K3.p, keys, (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess)
+      hipMemcpy(K3.p, keys, (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(KV3.p, keys, (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess)
     rc = rterr::set(RT_E_DEVICE, "upload");
   if (!rc) rc = S.sort({Seg{0, nn, depth < 0 ? 2 * lg2(nn) : depth, 0}});
   std::vector<uint32_t> dev(nn);
+  std::vector<float> dkv(nn);
   if (!rc && (hipStreamSynchronize(S.st) != hipSuccess ||
-              hipMemcpy(dev.data(), ids3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess))
+              hipMemcpy(dev.data(), ids3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(dkv.data(), KV3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess))
     rc = rterr::set(RT_E_DEVICE, "download");
   (void)hipStreamDestroy(S.st);
   if (rc) return rc;
   int64_t bad = 0;
-  for (uint32_t i = 0; i < nn; ++i) bad += dev[i] != host[i];
+  // a position counts once if its id differs from std::sort's or its carried
+  // key is not that id's key
+  for (uint32_t i = 0; i < nn; ++i)
+    bad += dev[i] != host[i] || dev[i] >= nn || std::memcmp(&dkv[i], &keys[dev[i] < nn ? dev[i] : 0], 4) != 0;
   *mismatch = bad;
   if (ids_out) std::memcpy(ids_out, dev.data(), (size_t)nn * 4);
   return RT_OK;
