@@ -879,27 +879,60 @@ struct PhaseTimer {
   }
 };
 
+// One device allocation for a whole build, carved into the build's buffers
+// (a hipMalloc / hipFree pair per buffer costs more than the launches of a
+// small stage). Buffers that outgrow their share fall back to hipMalloc.
+struct DevArena {
+  char *base = nullptr;
+  size_t cap = 0, off = 0;
+  ~DevArena() {
+    if (base) (void)hipFree(base);
+  }
+  static size_t round(size_t b) { return (b + 255) & ~(size_t)255; }
+  void *take(size_t bytes) {
+    if (!base || off + round(bytes) > cap) return nullptr;
+    void *q = base + off;
+    off += round(bytes);
+    return q;
+  }
+};
+thread_local DevArena *t_arena = nullptr;  // the arena of the build running on this thread
+
 template <class T>
 struct DBuf {
   T *p = nullptr;
   size_t cap = 0;
+  bool owned = false;
   ~DBuf() {
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
   }
+  static size_t first_cap(size_t n) { return std::max<size_t>(n, 1024); }  // what the first reserve(n) takes
   // grows geometrically: the per-stage buffers widen with the tree, and a
   // hipFree / hipMalloc pair at every stage for each of them synchronises the
   // device each time
   int reserve(size_t n) {
     if (n <= cap) return RT_OK;
     const size_t want = std::max<size_t>({n, 2 * cap, 1024});
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    owned = false;
+    if (t_arena)
+      if (void *q = t_arena->take(want * sizeof(T))) {
+        p = static_cast<T *>(q);
+        cap = want;
+        return RT_OK;
+      }
     HIP_TRY(hipMalloc(&p, want * sizeof(T)));
+    owned = true;
     cap = want;
     return RT_OK;
   }
 };
+template <class T>
+size_t dbytes(size_t n) {  // arena bytes of a DBuf<T> whose first reserve is n
+  return DevArena::round(DBuf<T>::first_cap(n) * sizeof(T));
+}
 
 // rtx_bvh_inject_failure: the next N device builds fail as a device error would
 std::atomic<int> g_inject_fail{0};
@@ -920,6 +953,14 @@ struct Sorter {
   PhaseTimer own_pt;             // per build: concurrent builds share no state
   PhaseTimer *pt = &own_pt;
 
+  // arena bytes of init(ntri)'s buffers (the same list)
+  static size_t arena_bytes(uint32_t ntri) {
+    const size_t N = 3 * (size_t)ntri, sercap = N / 2 + 4096, sc = N / (kSerialMax + 1) + 16,
+                 tc = N / kRoundTile + 2;
+    return 2 * dbytes<Seg>(sc) + dbytes<Seg>(sercap) + 2 * dbytes<uint32_t>(sc + 1) +
+           dbytes<uint32_t>(sc) + dbytes<float>(sc) + dbytes<uint32_t>(N) + dbytes<uint8_t>(N) +
+           dbytes<uint32_t>(2 * tc) + dbytes<uint32_t>(4 * sc) + 3 * dbytes<uint32_t>(N) + dbytes<uint32_t>(kCtlWords);
+  }
   int init(uint32_t ntri, uint32_t *ids3, float *kv3, const float *keys3) {
     n = ntri;
     ids = ids3;
@@ -1025,9 +1066,26 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     const hipError_t e_ = (expr);               \
     if (e_ != hipSuccess) return hfail(what, e_); \
   } while (0)
+  // wall time of the whole call, teardown included (RTAMD_BVH_TIMING)
+  struct WallClock {
+    bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), tv = t0, te = t0;
+    static double ms(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    }
+    ~WallClock() {
+      if (on) {
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[bvh gpu] wall %.1f ms (validation %.1f, teardown %.1f)\n", ms(t0, t1), ms(t0, tv),
+                     ms(te, t1));
+      }
+    }
+  } wall;
   if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
-  for (int64_t i = 0; i < nidx; ++i)
-    if ((int64_t)idx[i] >= nverts) { err = "vertex index out of range"; return false; }
+  uint32_t imax = 0;  // a max reduction vectorises; an early-exit loop does not
+  for (int64_t i = 0; i < nidx; ++i) imax = std::max(imax, idx[i]);
+  if (nidx && (int64_t)imax >= nverts) { err = "vertex index out of range"; return false; }
+  wall.tv = std::chrono::steady_clock::now();
   const uint32_t n = (uint32_t)(nidx / 3);
   if ((uint64_t)n > rtl::kMaxLeafFirstTri || 3ull * n >= (1ull << 31)) { err = "too many triangles"; return false; }
   out = BVHGpu();
@@ -1054,9 +1112,34 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   DBuf<float> ccost, dpsa;
   DBuf<uint32_t> cdivv;
   Sorter S;
+  // every buffer at its bound, from one allocation. Per stage: the candidates
+  // are disjoint ranges of > 8 triangles (tasks <= n / 9), each cut into
+  // chunks of kSahChunk on 3 axes; completed nodes' child ranges are disjoint
+  // (<= n); leaves <= n.
+  const size_t Tmax = n / 9 + 2, NCmax = 3 * (Tmax + n / kSahChunk + 2), NGmax = 3 * Tmax,
+               NRmax = (size_t)n + 1, NRCmax = NRmax + n / kSahChunk + 2, maxranges = 2 * (size_t)n + 8;
+  DevArena arena;
+  {
+    const size_t bytes = dbytes<float4>((size_t)nverts) + dbytes<uint32_t>((size_t)nidx) +
+                         dbytes<uint32_t>(3 * (size_t)n) + dbytes<uint32_t>(n) + 2 * dbytes<float>(3 * (size_t)n) +
+                         dbytes<TBox>(n) + Sorter::arena_bytes(n) + 2 * dbytes<uint32_t>(Tmax) +
+                         dbytes<Task>(Tmax) + dbytes<SahChunk>(NCmax) + dbytes<SahGroup>(NGmax) +
+                         3 * dbytes<TBox>(NCmax) + dbytes<float>(NCmax) + dbytes<uint32_t>(NCmax) +
+                         dbytes<float>(NGmax) + dbytes<TBox>(maxranges) + dbytes<SahChunk>(NRCmax) +
+                         dbytes<SahGroup>(NRmax) + dbytes<TBox>(NRCmax) + dbytes<uint32_t>(3 * (size_t)n);
+    BVH_DEV(hipMalloc(&arena.base, bytes), "allocation");
+    arena.cap = bytes;
+  }
+  struct ArenaScope {
+    explicit ArenaScope(DevArena *a) { t_arena = a; }
+    ~ArenaScope() { t_arena = nullptr; }
+  } arena_scope(&arena);
   if (dv.reserve((size_t)nverts) || didx.reserve((size_t)nidx) || ids3.reserve(3 * (size_t)n) ||
       backup.reserve(n) || K3.reserve(3 * (size_t)n) || KV3.reserve(3 * (size_t)n) || tbox.reserve(n) ||
-      S.init(n, ids3.p, KV3.p, K3.p))
+      S.init(n, ids3.p, KV3.p, K3.p) || dact.reserve(Tmax) || cdivv.reserve(NCmax) || dtasks.reserve(Tmax) ||
+      dchunks.reserve(NCmax) || dgroups.reserve(NGmax) || cbox.reserve(NCmax) || cpre.reserve(NCmax) ||
+      csuf.reserve(NCmax) || ccost.reserve(NCmax) || dpsa.reserve(NGmax) || boxes.reserve(maxranges) ||
+      drch.reserve(NRCmax) || drgrp.reserve(NRmax) || rcbox.reserve(NRCmax))
     return fail("allocation");
   S.pt = &pt;
   hipStream_t st = nullptr;
@@ -1214,6 +1297,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
                  pt.acc[7], pt.acc[5], pt.acc[0], pt.rounds, pt.acc[1], pt.serial_launches, pt.acc[2],
                  pt.acc[5] - pt.acc[0] - pt.acc[1] - pt.acc[2], pt.acc[6], pt.acc[3], pt.acc[4], pt.stages, pt.host[0],
                  pt.host[1], pt.host[2], pt.faults[0], pt.faults[1], pt.faults[2]);
+  wall.te = std::chrono::steady_clock::now();
   return true;
 #undef BVH_DEV
 }
