@@ -108,3 +108,30 @@ def gpu_frame(name, W, H, mode, pos=(0.0, 0.0, 2.5), clear=True, color=None, t=N
         t = np.full((H, W), np.inf, np.float32)
     s.render(params(name, W, H, mode, pos, "gpu"), color, t, clear=clear)
     return color, t
+
+
+def edge_mesh(seed, ntri, mode):
+    """test_host.py's tie-heavy triangle soups (vPos4f, one vertex per corner):
+    "same" duplicate triangles (all keys tie), "grid" integer lattices (many
+    equal keys), "flat" (zero-area boxes on one axis), "signed0" lattices whose
+    zero coordinates are a random mix of -0.0 and +0.0, "rand" small random
+    triangles."""
+    rng = np.random.default_rng(seed)
+    if mode == "signed0":
+        g = rng.integers(-2, 3, size=(ntri, 3)).astype(np.float64)
+        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
+        z = (v == 0) & (rng.random(v.shape) < 0.5)
+        v[z] = -0.0
+        assert np.signbit(v[v == 0]).any() and (~np.signbit(v[v == 0])).any()
+    elif mode == "same":
+        v = np.tile(rng.normal(size=(3, 3)), (ntri, 1))
+    elif mode == "grid":
+        g = rng.integers(0, 6, size=(ntri, 3)).astype(np.float64)
+        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
+    elif mode == "flat":
+        v = rng.normal(size=(ntri * 3, 3))
+        v[:, 1] = 0.25
+    else:
+        c = rng.normal(size=(ntri, 1, 3))
+        v = (c + 0.05 * rng.normal(size=(ntri, 3, 3))).reshape(-1, 3)
+    return np.concatenate([v, np.ones((len(v), 1))], axis=1).astype(np.float32)

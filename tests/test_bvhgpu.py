@@ -107,26 +107,8 @@ def test_device_builder_edge_meshes(gpu, seed, ntri, mode):
     box bound that is 0 must carry the sign bit calc_bbox gives it when the
     node is created (triangles_raytracing.cpp:199), before the children's
     sorts reorder the range."""
-    rng = np.random.default_rng(seed)
-    if mode == "signed0":
-        g = rng.integers(-2, 3, size=(ntri, 3)).astype(np.float64)
-        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
-        z = (v == 0) & (rng.random(v.shape) < 0.5)
-        v[z] = -0.0
-        assert np.signbit(v[v == 0]).any() and (~np.signbit(v[v == 0])).any()
-    elif mode == "same":
-        v = np.tile(rng.normal(size=(3, 3)), (ntri, 1))
-    elif mode == "grid":
-        g = rng.integers(0, 6, size=(ntri, 3)).astype(np.float64)
-        v = np.concatenate([g, g + [1, 0, 0], g + [0, 1, 0]], axis=1).reshape(-1, 3)
-    elif mode == "flat":
-        v = rng.normal(size=(ntri * 3, 3))
-        v[:, 1] = 0.25
-    else:
-        c = rng.normal(size=(ntri, 1, 3))
-        v = (c + 0.05 * rng.normal(size=(ntri, 3, 3))).reshape(-1, 3)
-    v4 = np.concatenate([v, np.ones((len(v), 1))], axis=1).astype(np.float32)
-    same_tree(v4, np.arange(len(v), dtype=np.uint32))
+    v4 = S.edge_mesh(seed, ntri, mode)
+    same_tree(v4, np.arange(len(v4), dtype=np.uint32))
 
 
 def test_device_builder_config5_standin(gpu):

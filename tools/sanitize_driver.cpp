@@ -19,6 +19,7 @@
 #include <tuple>
 #include <vector>
 
+#include "../triangles-sdf-cpu-raytracing_amd/csrc/rt_bvhstage.h"
 #include "../triangles-sdf-cpu-raytracing_amd/csrc/rt_host.h"
 
 namespace {
@@ -47,9 +48,17 @@ bool same_build(const char *name, const std::vector<float> &v, const std::vector
   }
   const bool same = a.canon == b.canon && a.perm_tri == b.perm_tri && a.max_depth == b.max_depth;
   check(same, std::string(name) + ": tree differs between 1 and " + std::to_string(threads) + " threads");
-  std::printf("%-28s %8zu tris  %7lld nodes  depth %d  %s\n", name, idx.size() / 3, (long long)b.host_nodes,
-              b.max_depth, same ? "same tree at 1 and N threads" : "DIFFERENT");
-  return same;
+  // the device builder's stage loop (rt_bvhstage.cpp, parallel passes) with
+  // its device steps emulated on the host
+  rth::BVHGpu e;
+  const bool emu = rth::bvhs::emulate_device_build(v.data(), (int64_t)v.size() / 4, idx.data(),
+                                                   (int64_t)idx.size(), e, err) &&
+                   e.canon == b.canon && e.perm_tri == b.perm_tri;
+  check(emu, std::string(name) + ": emulated device stage loop differs: " + err);
+  std::printf("%-28s %8zu tris  %7lld nodes  depth %d  %s%s\n", name, idx.size() / 3, (long long)b.host_nodes,
+              b.max_depth, same ? "same tree at 1 and N threads" : "DIFFERENT",
+              emu ? ", and from the device stage loop" : ", STAGE LOOP DIFFERS");
+  return same && emu;
 }
 
 // test_host.py's tie-heavy meshes: duplicate triangles, integer lattices, flat

@@ -1318,6 +1318,25 @@ int rtx_bvh_inject_failure(int32_t n) {
 // ids[] receives the device permutation; returns RT_OK and *mismatch = number
 // of positions that differ from the host permutation. depth < 0: std::sort's
 // own depth limit (2 lg n); smaller limits force the heapsort fallback.
+// The device builder's stage loop with the device steps done on the host
+// (rth::bvhs::emulate_device_build; no GPU needed): canonical export as
+// rt_bvh_export, `threads` OpenMP threads for the stage passes (0: default).
+int rtx_bvh_stage_emulate(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, uint32_t *canon,
+                          int64_t *nnodes) {
+  if (!vpos4 || !idx || !nnodes || nverts <= 0 || nidx <= 0) return rterr::set(RT_E_INVALID, "bad mesh");
+  rth::BVHGpu b;
+  std::string err;
+  if (!rth::bvhs::emulate_device_build(vpos4, nverts, idx, nidx, b, err, rth::kBvhCanon))
+    return rterr::set(RT_E_INVALID, err.c_str());
+  const int64_t nn = (int64_t)b.canon.size() / 52;
+  if (canon) {
+    if (*nnodes < nn) return rterr::set(RT_E_INVALID, "buffer too small");
+    std::memcpy(canon, b.canon.data(), b.canon.size() * 4);
+  }
+  *nnodes = nn;
+  return RT_OK;
+}
+
 int rtx_sort_check(const float *keys, int64_t n, int32_t depth, uint32_t *ids_out, int64_t *mismatch) {
   if (!keys || n <= 0 || n >= (1ll << 30) || !mismatch) return rterr::set(RT_E_INVALID, "bad arguments");
   const uint32_t nn = (uint32_t)n;

@@ -273,5 +273,131 @@ bool Stage::fifo(std::string &err) {
   return true;
 }
 
+
+// ---- the whole stage loop with the device steps emulated on the host --------
+namespace {
+
+struct EBox {
+  float mn[3], mx[3];
+};
+inline EBox e_empty() {
+  const float inf = __builtin_huge_valf();
+  return EBox{{inf, inf, inf}, {-inf, -inf, -inf}};
+}
+// tb_union of rt_bvhgpu.hip: the earlier operand is kept among equal bounds
+inline EBox e_union(const EBox &a, const EBox &b) {
+  EBox r;
+  for (int k = 0; k < 3; ++k) {
+    r.mn[k] = (b.mn[k] < a.mn[k]) ? b.mn[k] : a.mn[k];
+    r.mx[k] = (a.mx[k] < b.mx[k]) ? b.mx[k] : a.mx[k];
+  }
+  return r;
+}
+inline float e_area(const EBox &b) {
+  const float dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+  return 2 * (dx * dy + dx * dz + dy * dz);
+}
+
+}  // namespace
+
+bool emulate_device_build(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                          std::string &err, unsigned want) {
+  if (nidx < 0 || nidx % 3 != 0) { err = "index count must be a multiple of 3"; return false; }
+  for (int64_t i = 0; i < nidx; ++i)
+    if ((int64_t)idx[i] >= nverts) { err = "vertex index out of range"; return false; }
+  const uint32_t n = (uint32_t)(nidx / 3);
+  out = BVHGpu();
+  if (n == 0) { out.root_word = rtl::kInvalidChild; return true; }
+  constexpr uint32_t kChunk = 2048;  // kSahChunk
+  // k_tribox
+  std::vector<EBox> tb(n);
+  std::vector<float> K(3 * (size_t)n);
+  for (uint32_t t = 0; t < n; ++t) {
+    EBox b = e_empty();
+    for (int k = 0; k < 3; ++k) {
+      const float *v = vpos4 + 4 * (size_t)idx[3 * (size_t)t + k];
+      const float x = v[0] / v[3], y = v[1] / v[3], z = v[2] / v[3];
+      b = e_union(b, EBox{{x, y, z}, {x, y, z}});
+    }
+    tb[t] = b;
+    for (int a = 0; a < 3; ++a) K[(size_t)a * n + t] = b.mx[a];
+  }
+  std::vector<uint32_t> ids3(3 * (size_t)n), backup(n);
+  for (uint32_t t = 0; t < n; ++t) ids3[t] = t;
+  Stage SG;
+  if (!SG.init(n, kChunk)) { err = "host arrays"; return false; }
+  std::vector<float> hcc;
+  std::vector<uint32_t> hcd;
+  std::vector<EBox> right;
+  while (SG.n_open) {
+    const size_t r0 = SG.n_ranges;
+    SG.prologue();
+    const size_t T = SG.tasks.size();
+    if (T) {
+      for (const Task &tk : SG.tasks)  // k_stage_copy
+        for (uint32_t t = tk.s; t < tk.e; ++t) {
+          backup[t] = ids3[t];
+          ids3[n + t] = ids3[2 * (size_t)n + t] = ids3[t];
+        }
+      for (const Seg &sg : SG.segs)  // Sorter::sort: std::sort of each segment
+        host_introsort(ids3.data() + sg.first, sg.last - sg.first, K.data() + (size_t)(sg.first / n) * n, sg.depth);
+      // the chunked SAH sweeps: each chunk's first minimum over its dividers
+      hcc.assign(SG.ch.size(), __builtin_huge_valf());
+      hcd.assign(SG.ch.size(), 0xFFFFFFFFu);
+      for (size_t g = 0; g < SG.grp.size(); ++g) {
+        const Task tk = SG.tasks[g / 3];
+        const uint32_t *ids = ids3.data() + (g % 3) * (size_t)n;
+        right.assign((size_t)(tk.e - tk.s) + 1, e_empty());
+        for (uint32_t t = tk.e; t-- > tk.s;) right[t - tk.s] = e_union(tb[ids[t]], right[t - tk.s + 1]);
+        const float psa = e_area(right[0]);
+        EBox left = e_empty();
+        const SahGroup G = SG.grp[g];
+        for (uint32_t k = G.first; k < G.first + G.count; ++k) {
+          const SahChunk c = SG.ch[k];
+          float best = __builtin_huge_valf();
+          uint32_t bdiv = 0xFFFFFFFFu;
+          for (uint32_t t = c.lo; t < c.hi; ++t) {
+            const uint32_t d = t + 1;
+            left = e_union(left, tb[ids[t]]);
+            if (d >= tk.e) continue;
+            const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
+            const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
+            const float cost = 0.2f + e_area(left) / psa * lc + e_area(right[d - tk.s]) / psa * rc;
+            if (cost < best) {
+              best = cost;
+              bdiv = d;
+            }
+          }
+          hcc[k] = best;
+          hcd[k] = bdiv;
+        }
+      }
+      SG.reduce_sah(hcc.data(), hcd.data());
+    }
+    if (!SG.fifo(err)) return false;
+    for (size_t ti = 0; ti < T; ++ti) {  // k_stage_apply
+      const uint32_t a = SG.action[ti];
+      if (a == 0) continue;
+      const Task tk = SG.tasks[ti];
+      for (uint32_t t = tk.s; t < tk.e; ++t)
+        ids3[t] = a == 1 ? ids3[n + t] : a == 2 ? ids3[2 * (size_t)n + t] : backup[t];
+    }
+    for (size_t r = r0; r < SG.n_ranges; ++r) {  // child boxes over the order after the apply
+      const Task R = SG.ranges[r];
+      EBox b = e_empty();
+      for (uint32_t t = R.s; t < R.e; ++t) b = e_union(b, tb[ids3[t]]);
+      BvhBox &dst = SG.H[SG.range_of[r].first].box[SG.range_of[r].second];
+      for (int k = 0; k < 3; ++k) {
+        dst.mn[k] = b.mn[k];
+        dst.mx[k] = b.mx[k];
+      }
+    }
+    SG.advance();
+  }
+  const std::vector<uint32_t> cur(ids3.begin(), ids3.begin() + n);
+  bvh_layout(vpos4, idx, nidx, HostNodes(SG.H.p, SG.n_nodes), cur, out, want, true);
+  return true;
+}
+
 }  // namespace bvhs
 }  // namespace rth

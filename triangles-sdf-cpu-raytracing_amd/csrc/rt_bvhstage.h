@@ -111,5 +111,12 @@ struct Stage {
   std::vector<uint32_t> a_, b_, kind_;  // per open node scratch
 };
 
+// The device builder's stage loop with its device steps done on the host
+// (stage copies, std::sort of every segment, the chunked SAH sweeps, the
+// apply, child boxes): checks the host half (prologue / reduce_sah / fifo, in
+// parallel) against the host builder on machines without a GPU, and under
+// the sanitizers. Same tree as build_bvh8.
+bool emulate_device_build(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx, BVHGpu &out,
+                          std::string &err, unsigned want = kBvhAll);
 }  // namespace bvhs
 }  // namespace rth
