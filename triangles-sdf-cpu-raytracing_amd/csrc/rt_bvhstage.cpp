@@ -156,7 +156,8 @@ bool Stage::fifo(std::string &err) {
   a_.resize(no + 1);  // next-list entries per open node
   b_.resize(no + 1);  // new nodes (= child ranges) per open node
   // pass 1: the FIFO of each node, candidate by candidate (:162-173)
-#pragma omp parallel for schedule(static) if (no >= kParMin)
+  int overflow = 0;  // a queue past 8 candidates (cannot happen: see OpenState)
+#pragma omp parallel for schedule(static) if (no >= kParMin) reduction(| : overflow)
   for (size_t o = 0; o < no; ++o) {
     OpenState &N = OS[open[o]];
     Cand q2[8];
@@ -201,6 +202,8 @@ bool Stage::fifo(std::string &err) {
         if (qn2 + 2 <= 8) {
           q2[qn2++] = Cand{start, dv3[win]};
           q2[qn2++] = Cand{dv3[win], end};
+        } else {
+          overflow = 1;
         }
       }
     }
@@ -226,6 +229,10 @@ bool Stage::fifo(std::string &err) {
     std::sort(N.div, N.div + N.nd);
     kind_[o] = 2;
     a_[o] = b_[o] = (uint32_t)N.nd + 1;
+  }
+  if (overflow) {
+    err = "candidate queue bound";
+    return false;
   }
   const size_t nn = excl_scan(a_, no), nc = excl_scan(b_, no);
   if (n_nodes + nc > H.cap || n_ranges + nc > ranges.cap || nn > next.cap) {

@@ -494,6 +494,12 @@ struct PersistQ {
   uint32_t waves;    // waves in the grid
   uint32_t gx, gy;   // wave tiles (8x8 pixels) per item: 1x1, 2x1 or 2x2
   uint32_t stride;   // words between heads
+  // item order of a head (render_persist_kernel): cpf == 0 interleaved (item
+  // i on head i % 8); cpf > 0 banded: head h takes tile rows [h cpf, (h+1) cpf)
+  // of the row-major items of every frame, frame after frame (nper = frames x
+  // cpf slots, slots past per_frame are empty), so an XCD's L2 holds the part
+  // of the scene its band of the image sees; a drained head steals as before
+  uint32_t cpf, nper;
   // diagnostic builds (-DRT_PERSIST_STAMPS, tools/build_variant.sh; see
   // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 8 x u64 =
   // start, end (s_memrealtime, 100 MHz), items traced | XCD << 32, end of its
@@ -540,15 +546,30 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
   uint32_t k = q_claim(q.heads + h * q.stride);
   NoCnt cnt{};
   for (;;) {
-    const uint32_t item = k * 8 + h;
-    if (item >= q.items) {
+    // slot k of head h -> item (frame f, row-major index r in the frame)
+    uint32_t item, f, r;
+    bool drained, empty = false;
+    if (q.cpf == 0) {
+      item = k * 8 + h;
+      drained = item >= q.items;
+      f = item / q.per_frame;
+      r = item - f * q.per_frame;
+    } else {
+      drained = k >= q.nper;
+      f = k / q.cpf;
+      r = h * q.cpf + (k - f * q.cpf);
+      empty = r >= q.per_frame;
+      item = f * q.per_frame + r;
+    }
+    if (drained) {
       // head h drained: read all eight heads at once (lanes 0-7, one round
       // trip) and claim from a head that still has items, the first one after
       // this XCD's own; none left: done. A claim that loses the race to the
       // last item just comes back here.
       uint32_t v = 0xFFFFFFFFu;
       if (lane < 8) v = __hip_atomic_load(q.heads + lane * q.stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t m = __ballot(lane < 8 && v < (q.items + 7u - (uint32_t)lane) / 8u) & 0xFFull;
+      const uint32_t cap = q.cpf ? q.nper : (q.items + 7u - (uint32_t)lane) / 8u;
+      const uint64_t m = __ballot(lane < 8 && v < cap) & 0xFFull;
       if (m == 0) break;
       const uint32_t rot = (uint32_t)(((m >> (xcc + 1)) | (m << (7 - xcc))) & 0xFFull);  // bit i: head xcc+1+i
       h = (xcc + 1 + (uint32_t)__builtin_ctz(rot)) & 7u;
@@ -556,7 +577,10 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
       continue;
     }
     const uint32_t knext = q_claim(q.heads + h * q.stride);
-    const uint32_t f = item / q.per_frame, r = item - f * q.per_frame;
+    if (empty) {
+      k = knext;
+      continue;
+    }
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
 #ifdef RT_PERSIST_STAMPS
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1297,6 +1321,13 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   q.tiles_x = (uint32_t)((fb.f[0].W + 8 * q.gx - 1) / (8 * q.gx));
   q.per_frame = q.tiles_x * (uint32_t)((fb.f[0].rows_local + 8 * q.gy - 1) / (8 * q.gy));
   q.items = q.per_frame * (uint32_t)n;
+  // RTAMD_QMAP=band: banded item order per head (PersistQ::cpf)
+  static const bool banded = [] {
+    const char *e = std::getenv("RTAMD_QMAP");
+    return e && std::strcmp(e, "band") == 0;
+  }();
+  q.cpf = banded ? (q.per_frame + 7) / 8 : 0;
+  q.nper = q.cpf * (uint32_t)n;
   grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
   q.waves = grid * (kBlock / 64);
   q.stamps = (g_persist_stamps && (int64_t)q.waves <= g_persist_stamps_cap) ? g_persist_stamps : nullptr;
