@@ -51,7 +51,7 @@ using rth::bvhs::Seg;
 using rth::bvhs::Task;
 
 #ifndef RT_SERIAL_MAX
-#define RT_SERIAL_MAX 256  // A/B switch
+#define RT_SERIAL_MAX 1024  // A/B switch (256: 2.9 ms short sorts + 14.9 ms rounds; 1024: 5.7 + 10.3, 1.1 M tris)
 #endif
 constexpr uint32_t kSerialMax = RT_SERIAL_MAX;  // segments at most this long: one wave, serial introsort in LDS
 
@@ -656,170 +656,6 @@ __global__ __launch_bounds__(kSahT) void k_sah_chunk_box(const SahChunk *chunks,
   if (threadIdx.x == 0) cbox[blockIdx.x] = sm[0];
 }
 
-// ---- the same two kernels by waves ------------------------------------------
-// A wave takes 512 consecutive triangles of the chunk as 8 rows of 64 (lane =
-// triangle: coalesced id loads) and scans boxes across its lanes with
-// shuffles; unions always take the earlier operand first, so every fold keeps
-// the first of equal bounds as the sequential sweep does. RTAMD_SAH=block
-// selects the LDS block-scan kernels above.
-__device__ __forceinline__ TBox tb_shfl_down(const TBox &x, int d) {
-  TBox r;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    r.mn[k] = __shfl_down(x.mn[k], d, 64);
-    r.mx[k] = __shfl_down(x.mx[k], d, 64);
-  }
-  return r;
-}
-__device__ __forceinline__ TBox tb_shfl_up(const TBox &x, int d) {
-  TBox r;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    r.mn[k] = __shfl_up(x.mn[k], d, 64);
-    r.mx[k] = __shfl_up(x.mx[k], d, 64);
-  }
-  return r;
-}
-__device__ __forceinline__ TBox tb_lane(const TBox &x, int l) {
-  TBox r;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    r.mn[k] = __shfl(x.mn[k], l, 64);
-    r.mx[k] = __shfl(x.mx[k], l, 64);
-  }
-  return r;
-}
-// union of this lane's box and every later lane's (lane 0: the whole wave)
-__device__ __forceinline__ TBox wave_suffix_incl(TBox x, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const TBox y = tb_shfl_down(x, d);
-    if (lane + d < 64) x = tb_union(x, y);
-  }
-  return x;
-}
-// union of every lane's box up to and including this one
-__device__ __forceinline__ TBox wave_prefix_incl(TBox x, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const TBox y = tb_shfl_up(x, d);
-    if (lane >= (uint32_t)d) x = tb_union(y, x);
-  }
-  return x;
-}
-constexpr int kSahW = kSahT / 64, kSahRows = kSahChunk / kSahT;  // waves per block, rows of 64 per wave
-
-__global__ __launch_bounds__(kSahT) void k_sah_chunk_box_w(const SahChunk *chunks, const uint32_t *ids3,
-                                                           const TBox *tbox, uint32_t n, TBox *cbox) {
-  __shared__ TBox wt[kSahW];
-  const SahChunk c = chunks[blockIdx.x];
-  const uint32_t *ids = ids3 + c.axis * n;
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u, wb = c.lo + w * (64 * kSahRows);
-  TBox acc = tb_empty();
-#pragma unroll
-  for (int q = 0; q < kSahRows; ++q) {
-    const uint32_t t = wb + q * 64 + lane;
-    const TBox row = wave_suffix_incl(t < c.hi ? tbox[ids[t]] : tb_empty(), lane);
-    acc = tb_union(acc, tb_lane(row, 0));
-  }
-  if (lane == 0) wt[w] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    TBox a = wt[0];
-    for (int k = 1; k < kSahW; ++k) a = tb_union(a, wt[k]);
-    cbox[blockIdx.x] = a;
-  }
-}
-
-__global__ __launch_bounds__(kSahT) void k_sah_chunk_cost_w(const SahChunk *chunks, const Task *tasks,
-                                                            const uint32_t *ids3, const TBox *tbox, uint32_t n,
-                                                            const TBox *cpre, const TBox *csuf, const float *psa_g,
-                                                            float *ccost, uint32_t *cdiv) {
-  __shared__ TBox rowt[kSahW][kSahRows];  // each row's union
-  __shared__ TBox wt[kSahW];              // each wave's union
-  __shared__ float s_cost[kSahW];
-  __shared__ uint32_t s_div[kSahW];
-  const SahChunk c = chunks[blockIdx.x];
-  const Task tk = tasks[c.task];
-  const uint32_t *ids = ids3 + c.axis * n;
-  const float psa = psa_g[c.group];
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u, wb = c.lo + w * (64 * kSahRows);
-  TBox tb[kSahRows];
-#pragma unroll
-  for (int q = 0; q < kSahRows; ++q) {
-    const uint32_t t = wb + q * 64 + lane;
-    tb[q] = t < c.hi ? tbox[ids[t]] : tb_empty();
-  }
-  // right boxes (everything after triangle t): a suffix scan per row, then the
-  // rows after it, the waves after this one and the chunks after this one
-  TBox rsuf[kSahRows];
-  TBox wtot = tb_empty();
-#pragma unroll
-  for (int q = kSahRows - 1; q >= 0; --q) {
-    rsuf[q] = wave_suffix_incl(tb[q], lane);
-    const TBox rt = tb_lane(rsuf[q], 0);
-    if (lane == 0) rowt[w][q] = rt;
-    wtot = tb_union(rt, wtot);
-  }
-  if (lane == 0) wt[w] = wtot;
-  __syncthreads();
-  TBox after = csuf[blockIdx.x];  // waves after this one, then the chunks after
-  for (int k = kSahW - 1; k > (int)w; --k) after = tb_union(wt[k], after);
-  float rarea[kSahRows];
-#pragma unroll
-  for (int q = kSahRows - 1; q >= 0; --q) {
-    const TBox sh = tb_shfl_down(rsuf[q], 1);
-    const TBox ex = lane < 63 ? sh : tb_empty();
-    rarea[q] = tb_area(tb_union(ex, after));
-    after = tb_union(rowt[w][q], after);
-  }
-  // left boxes (everything up to and including t): chunks before, waves
-  // before, rows before, then a prefix scan of the row
-  TBox before = cpre[blockIdx.x];
-  for (int k = 0; k < (int)w; ++k) before = tb_union(before, wt[k]);
-  float best = __builtin_huge_valf();
-  uint32_t bdiv = 0xFFFFFFFFu;
-#pragma unroll
-  for (int q = 0; q < kSahRows; ++q) {
-    const TBox left = tb_union(before, wave_prefix_incl(tb[q], lane));
-    const uint32_t t = wb + q * 64 + lane, d = t + 1;  // divider after triangle t (index units: 3 d)
-    if (t < c.hi && d < tk.e) {
-      const float lc = static_cast<float>(3u * (d - tk.s)) / 3.0f;
-      const float rc = static_cast<float>(3u * (tk.e - tk.s)) / 3.0f - lc;
-      const float cost = 0.2f + tb_area(left) / psa * lc + rarea[q] / psa * rc;
-      if (cost < best) {  // NaN never wins; a lane's dividers ascend
-        best = cost;
-        bdiv = d;
-      }
-    }
-    before = tb_union(before, rowt[w][q]);
-  }
-  // first minimum, lexicographic (cost, divider): the wave, then the block
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const float c2 = __shfl_xor(best, d, 64);
-    const uint32_t d2 = (uint32_t)__shfl_xor((int)bdiv, d, 64);
-    if (c2 < best || (c2 == best && d2 < bdiv)) {
-      best = c2;
-      bdiv = d2;
-    }
-  }
-  if (lane == 0) {
-    s_cost[w] = best;
-    s_div[w] = bdiv;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < kSahW; ++k)
-      if (s_cost[k] < best || (s_cost[k] == best && s_div[k] < bdiv)) {
-        best = s_cost[k];
-        bdiv = s_div[k];
-      }
-    ccost[blockIdx.x] = best;
-    cdiv[blockIdx.x] = bdiv;
-  }
-}
-
 // one thread per (candidate, axis): exclusive prefix / suffix unions of its
 // chunks, and the parent's surface area (:84, the union of the whole range)
 __global__ void k_sah_carry(const SahGroup *groups, uint32_t ng, const TBox *cbox, TBox *cpre, TBox *csuf,
@@ -1331,10 +1167,6 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   // come out as the reference's sequential min / max)
   bvhs::Stage SG;
   if (!SG.init(n, kSahChunk)) return hfail("host arrays", hipErrorOutOfMemory);
-  static const bool sah_wave = [] {  // RTAMD_SAH=block: the LDS block-scan SAH kernels
-    const char *e = std::getenv("RTAMD_SAH");
-    return !(e && std::strcmp(e, "block") == 0);
-  }();
   if (boxes.reserve(SG.ranges.cap)) return fail("allocation");
   std::vector<float> hcc;
   std::vector<uint32_t> hcd;
@@ -1359,15 +1191,10 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       pt.hstop(0);
       if (S.sort(SG.segs)) return fail("sort");
       pt.start();
-      if (sah_wave) k_sah_chunk_box_w<<<NC, kSahT, 0, st>>>(dchunks.p, ids3.p, tbox.p, n, cbox.p);
-      else k_sah_chunk_box<<<NC, kSahT, 0, st>>>(dchunks.p, ids3.p, tbox.p, n, cbox.p);
+      k_sah_chunk_box<<<NC, kSahT, 0, st>>>(dchunks.p, ids3.p, tbox.p, n, cbox.p);
       k_sah_carry<<<(NG + 63) / 64, 64, 0, st>>>(dgroups.p, NG, cbox.p, cpre.p, csuf.p, dpsa.p);
-      if (sah_wave)
-        k_sah_chunk_cost_w<<<NC, kSahT, 0, st>>>(dchunks.p, dtasks.p, ids3.p, tbox.p, n, cpre.p, csuf.p, dpsa.p,
-                                                 ccost.p, cdivv.p);
-      else
-        k_sah_chunk_cost<<<NC, kSahT, 0, st>>>(dchunks.p, dtasks.p, ids3.p, tbox.p, n, cpre.p, csuf.p, dpsa.p,
-                                               ccost.p, cdivv.p);
+      k_sah_chunk_cost<<<NC, kSahT, 0, st>>>(dchunks.p, dtasks.p, ids3.p, tbox.p, n, cpre.p, csuf.p, dpsa.p, ccost.p,
+                                             cdivv.p);
       BVH_DEV(hipGetLastError(), "SAH sweep");
       hcc.resize(NC);
       hcd.resize(NC);
@@ -1403,8 +1230,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
       if (drch.reserve(nrc) || drgrp.reserve(nr) || rcbox.reserve(nrc)) return fail("allocation");
       BVH_DEV(hipMemcpyAsync(drch.p, rch.data(), nrc * sizeof(SahChunk), hipMemcpyHostToDevice, st), "upload");
       BVH_DEV(hipMemcpyAsync(drgrp.p, rgrp.data(), nr * sizeof(SahGroup), hipMemcpyHostToDevice, st), "upload");
-      if (sah_wave) k_sah_chunk_box_w<<<nrc, kSahT, 0, st>>>(drch.p, ids3.p, tbox.p, n, rcbox.p);
-      else k_sah_chunk_box<<<nrc, kSahT, 0, st>>>(drch.p, ids3.p, tbox.p, n, rcbox.p);
+      k_sah_chunk_box<<<nrc, kSahT, 0, st>>>(drch.p, ids3.p, tbox.p, n, rcbox.p);
       k_group_fold<<<(nr + 63) / 64, 64, 0, st>>>(drgrp.p, nr, rcbox.p, boxes.p + r0);
       BVH_DEV(hipGetLastError(), "child boxes");
     }
