@@ -4,7 +4,9 @@ the same frames as the one-frame render_kernel and as the oracle, bit for bit:
 every refill threshold, frame sizes with partial tiles and fewer pixels than
 the grid has lanes, tPrev accumulation (no clear), cameras whose rays have
 zero direction components (the exact slab form), and 8 frames of different
-cameras mixed in one launch (lanes of one wave on different frames)."""
+cameras mixed in one launch (lanes of one wave on different frames). The
+octrees and the SDF grid (linear 65^3 and the bricked 256^3 stand-in) are
+pumped."""
 import os
 import subprocess
 import sys
@@ -17,7 +19,7 @@ import scenes as S
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PUMPED = ["sdf_6.octree", "sdf_5.octree"]
+PUMPED = ["sdf_6.octree", "sdf_5.octree", "example_grid.grid"]
 
 
 def pump(sc, on=True):
@@ -140,6 +142,32 @@ def test_pump_refill_thresholds(gpu, refill):
         "import torch, test_pump as T, scenes as S\n"
         "sc = S.gpu_scene('sdf_6.octree'); sc.set_plane(None)\n"
         "prm = T.cams(160, 96, 8, seed=4)\n"
+        "T.same(T.batch(sc, prm, 160, 96), T.single(sc, prm, 160, 96), 'refill')\n"
+        "print('ok')\n" % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                           os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RTAMD_REFILL=refill, RTAMD_PUMP="1"),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_pump_bricked_grid_stand_in(gpu):
+    """The 256^3 stand-in (configs[2]; bricked layout, buffer loads) on the
+    pump equals the one-frame path."""
+    from rtamd import workloads as WL
+    sc, _ = WL.scene_for("grid")
+    sc.set_plane(None)
+    W, H = 256, 144
+    prm = cams(W, H, 8, seed=7)
+    same(batch(sc, prm, W, H), single(sc, prm, W, H), "grid 256^3")
+
+
+@pytest.mark.parametrize("refill", ["1", "32", "64"])
+def test_pump_grid_refill_thresholds(gpu, refill):
+    code = (
+        "import sys; sys.path[:0] = [%r, %r, %r]\n"
+        "import torch, test_pump as T, scenes as S\n"
+        "sc = S.gpu_scene('example_grid.grid'); sc.set_plane(None)\n"
+        "prm = T.cams(160, 96, 8, seed=5)\n"
         "T.same(T.batch(sc, prm, 160, 96), T.single(sc, prm, 160, 96), 'refill')\n"
         "print('ok')\n" % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
                            os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd")))

@@ -703,6 +703,29 @@ struct OctP {
   }
 };
 
+// the grid's sphere march on the pump (grid_start / grid_run): a lane's state
+// is (t, p), so a refill costs an eye ray and a box entry
+template <int kMode>
+struct GridP {
+  using Ray = GridRay;
+  static constexpr int kFields = 1;  // no traversal stack (one unused LDS word per lane)
+  static constexpr int kMinWaves = RT_GRID_WAVES;
+  GridDev d;
+  template <bool FAST>
+  __device__ __forceinline__ int start(f3 o, f3 dir, f3 inv, float tf, Ray &R, float &, f3 &) const {
+    return grid_start(o, dir, inv, 0.01f, tf, R);
+  }
+  template <bool FAST>
+  __device__ __forceinline__ int run(f3 o, f3 dir, f3, float, LdsStack<kBlock, kFields>, Ray &R, int limit,
+                                     float &t, f3 &n) const {
+    NoCnt c;
+    f3 hp;
+    const int s = grid_run<kMode, true>(d, o, dir, R, limit, t, hp, c);
+    if (s == RAY_HIT) n = grid_normal<kMode>(d, hp, c);
+    return s;
+  }
+};
+
 #ifndef RT_REFILL_MIN
 #define RT_REFILL_MIN 16  // dead lanes that trigger a refill (RTAMD_REFILL overrides)
 #endif
@@ -1377,6 +1400,16 @@ struct PumpOf<OctS<PK>> {
   using P = OctP;
   static P make(const OctS<PK> &s) { return P{s.d}; }
 };
+template <int kMode>
+struct PumpOf<GridS<kMode>> {
+  static constexpr bool kHas = true;
+  using P = GridP<kMode>;
+  static P make(const GridS<kMode> &s) { return P{s.d}; }
+};
+// work-queue item of the pump for scenes that otherwise take the block
+// dispatch (the grid): 2x2 wave tiles, so a wave's pixel stream claims once per
+// 256 pixels
+constexpr int kPumpGroup = 4;
 
 template <class P, int MAXD>
 int launch_pump_t(const P &sc, const FrameBatch &fb, int n, int group, hipStream_t stream) {
@@ -1395,11 +1428,13 @@ int launch_batch_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatc
   // Row-band tiles (a rank's share of a multi-GPU frame) with fewer than about
   // a million pixels take the block dispatch (band_takes_queue).
   const int group = persist_group(S::kQueueGroup);
+  if constexpr (PumpOf<S>::kHas) {
+    if (!general && (pump_env() || (s && s->pump_on)) && persist_enabled() && band_takes_queue(fb.f[0]))
+      return launch_pump_t<typename PumpOf<S>::P, MAXD>(PumpOf<S>::make(sc), fb, n,
+                                                        persist_group(S::kQueueGroup ? S::kQueueGroup : kPumpGroup),
+                                                        stream);
+  }
   if (persist_enabled() && group > 0 && band_takes_queue(fb.f[0])) {
-    if constexpr (PumpOf<S>::kHas) {
-      if (!general && (pump_env() || (s && s->pump_on)))
-        return launch_pump_t<typename PumpOf<S>::P, MAXD>(PumpOf<S>::make(sc), fb, n, group, stream);
-    }
     return general ? launch_persist_t<S, MAXD, true>(s, sc, pl, fb, n, group, stream)
                    : launch_persist_t<S, MAXD, false>(s, sc, pl, fb, n, group, stream);
   }

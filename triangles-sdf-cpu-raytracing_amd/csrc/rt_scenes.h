@@ -943,6 +943,9 @@ __device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  //
   return normalize(f3{dx, dy, dz});
 }
 
+// ray status: still traversing (suspended), finished without a hit, with a hit
+enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
+
 // grid_raytracing.cpp:93-125. Returns hit and leaves the hit point in *hp.
 template <int kMode, class CT>
 __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
@@ -991,6 +994,52 @@ __device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, floa
   f3 p;
   uint32_t cell;
   return grid_march<kMode>(g, o, d, tNear, tFar, t, p, cell, cnt);
+}
+
+// SDFGrid::intersect (grid_raytracing.cpp:93-125) split for the ray pump
+// (render_pump_kernel): grid_start is the box entry and the clamp of the first
+// march point, grid_run the sphere march, which can suspend between two steps
+// and continue later in the same lane. The state between steps is the
+// reference's (t, p) pair; the tap cache is not carried over (a resumed step
+// reloads its 8 taps: the same samples, the same bits).
+struct GridRay {
+  float t;
+  f3 p;
+};
+__device__ __forceinline__ int grid_start(f3 o, f3 d, f3 inv, float tNear, float tFar, GridRay &R) {
+  float t1, t2;
+  bbox_intersection(f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, inv, tNear, tFar, t1, t2);
+  if (t1 > t2) return RAY_MISS;
+  f3 p = o + t1 * d;
+  p = vstd_max(p, f3{-1.0f, -1.0f, -1.0f});
+  p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
+  R = GridRay{t1, p};
+  return RAY_PENDING;
+}
+// SUSPEND: before each step, if `limit` or fewer lanes of the wave are still
+// marching, save (t, p) and return RAY_PENDING.
+template <int kMode, bool SUSPEND, class CT>
+__device__ __forceinline__ int grid_run(const GridDev &g, f3 o, f3 d, GridRay &R, int limit, float &out_t,
+                                        f3 &hp, CT &cnt) {
+  float t = R.t;
+  f3 p = R.p;
+  GridTaps tc;
+  uint32_t cell;
+  while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
+    if (SUSPEND && __popcll(__ballot(1)) <= limit) {
+      R = GridRay{t, p};
+      return RAY_PENDING;
+    }
+    const float s = grid_sdf_t<kMode, RT_GRID_TAP_CACHE != 0>(g, p, &cell, tc, cnt);
+    if (s < 1e-3f) {
+      out_t = t + s;
+      hp = p;
+      return RAY_HIT;
+    }
+    t += s;
+    p = o + t * d;
+  }
+  return RAY_MISS;
 }
 
 // ----------------------------------------------------------------- octree --
@@ -1311,8 +1360,6 @@ struct OctRay {
   int32_t depth;  // depth of the top frame's node (root = 0)
   int32_t sp;     // frames on the LDS stack
 };
-// ray status: still traversing (suspended), finished without a hit, with a hit
-enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 
 // SDFOctree::intersect -> intersectNode(0) (octree_raytracing.cpp:166-208), root stage.
 template <bool FAST, class CT>
