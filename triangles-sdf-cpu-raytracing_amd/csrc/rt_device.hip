@@ -41,6 +41,18 @@ namespace {
 inline int set_err(int code, const std::string &msg) { return rterr::set(code, msg); }
 
 constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
+// Workgroup of the persistent multi-frame kernel (render_persist_kernel), in
+// threads. Its waves are independent (each pulls its own items), so the block
+// only sets the granularity at which a launch's resources are handed back:
+// the next launch on the other stream gets a workgroup slot only when every
+// wave of a finished workgroup has left. One wave per workgroup lets the next
+// launch replace the draining one wave by wave (128 and
+// 256, the block-dispatch size, are A/B settings).
+#ifndef RT_PERSIST_BLOCK
+#define RT_PERSIST_BLOCK 64
+#endif
+constexpr int kPBlock = RT_PERSIST_BLOCK;
+static_assert(kPBlock % 64 == 0 && kPBlock >= 64 && kPBlock <= 1024, "persistent block: whole waves");
 constexpr int kTile = 16;
 
 struct FrameArgs {
@@ -320,7 +332,7 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 // 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
 
 // One pixel per lane of the wave's 8x8 tile: column xo, rank-local row yl.
-template <class S, int SLOTS, bool GENERAL, int DIAG, class CT>
+template <class S, int SLOTS, bool GENERAL, int DIAG, int B = kBlock, class CT>
 __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
                                               CT &cnt, uint32_t *stk, int xo, int yl) {
   const bool active = xo < fa.W && yl < fa.rows_local;
@@ -328,7 +340,7 @@ __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, c
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
   if (DIAG == 0 && !kWaveCoop && !active) return;
   if (active || kWaveCoop) {  // (the counting variant keeps every lane for its wave reduction)
-    LdsStack<kBlock, S::kFields> st{stk + threadIdx.x};
+    LdsStack<B, S::kFields> st{stk + threadIdx.x};
     const int yo = image_row(active ? yl : 0, fa);
     const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
     const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
@@ -351,16 +363,16 @@ __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, c
       cnt.add(C_RAYS, 1);
       Hit h;
       if constexpr (kWaveCoop)
-        h = sc.template primary<kBlock>(o, d, 0.01f, tFarEff, active, stk);
+        h = sc.template primary<B>(o, d, 0.01f, tFarEff, active, stk);
       else
-        h = sc.template intersect<kBlock>(o, d, 0.01f, tFarEff, st, cnt);
+        h = sc.template intersect<B>(o, d, 0.01f, tFarEff, st, cnt);
       hit = h.hit;
       t = h.t;
       f3 n = h.n;
       if (dot(n, d) > 0) n = n * -1.0f;
       c = f4{(n.x + 1.0f) / 2.0f, (n.y + 1.0f) / 2.0f, (n.z + 1.0f) / 2.0f, (1.0f + 1.0f) / 2.0f};
     } else {
-      c = shade_one<S, kBlock>(sc, pl, fa.P, o, d, tFarEff, true, hit, t, st, nullptr, cnt);
+      c = shade_one<S, B>(sc, pl, fa.P, o, d, tFarEff, true, hit, t, st, nullptr, cnt);
     }
     // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
     const bool store = hit && !__builtin_isinf(t);
@@ -501,7 +513,7 @@ struct PersistQ {
   // of the scene its band of the image sees; a drained head steals as before
   uint32_t cpf, nper;
   // diagnostic builds (-DRT_PERSIST_STAMPS, tools/build_variant.sh; see
-  // rtx_set_persist_stamps): per wave w = blockIdx.x * 4 + wave, 8 x u64 =
+  // rtx_set_persist_stamps): per wave w = blockIdx.x * (kPBlock / 64) + wave, 8 x u64 =
   // start, end (s_memrealtime, 100 MHz), items traced | XCD << 32, end of its
   // last item, start of its last item, last item, longest item's duration, longest item
   unsigned long long *stamps;
@@ -519,9 +531,9 @@ __device__ __forceinline__ uint32_t q_claim(uint32_t *head) {
 }
 
 template <class S, int SLOTS, bool GENERAL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
+__global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, 0>())))
 void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
-  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
+  __shared__ uint32_t stk[SLOTS * S::kFields * kPBlock];
   S sc = sc_arg;
   if constexpr (S::kLdsNodes > 0 && !GENERAL) {
     // the top BVH levels (the first inner nodes, BFS order) copied into this
@@ -530,7 +542,7 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
     __shared__ float4 lnodes[S::kLdsNodes * kQ];
     const uint32_t n = sc.d.n_inner < (uint32_t)S::kLdsNodes ? sc.d.n_inner : (uint32_t)S::kLdsNodes;
     const float4 *src = reinterpret_cast<const float4 *>(sc.d.nodes);
-    for (uint32_t i = threadIdx.x; i < n * kQ; i += kBlock) lnodes[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < n * kQ; i += kPBlock) lnodes[i] = src[i];
     __syncthreads();
     sc.d.lnodes = reinterpret_cast<const rtl::GNode *>(lnodes);
     sc.d.n_lds = n;
@@ -593,7 +605,7 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
         // live across the traversal
         uint32_t fo = f;
         asm volatile("" : "+s"(fo));
-        render_pixels<S, SLOTS, GENERAL, 0>(sc, pl, fb.f[fo], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
+        render_pixels<S, SLOTS, GENERAL, 0, kPBlock>(sc, pl, fb.f[fo], cnt, stk, (int)((tx * q.gx + i) * 8) + (lane & 7),
                                             (int)((ty * q.gy + j) * 8) + (lane >> 3));
       }
 #ifdef RT_PERSIST_STAMPS
@@ -610,7 +622,7 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
   }
 #ifdef RT_PERSIST_STAMPS
   if (q.stamps && lane == 0) {
-    const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const size_t w = (size_t)blockIdx.x * (kPBlock / 64) + (threadIdx.x >> 6);
     unsigned long long *o = q.stamps + 8 * w;
     o[0] = t_start;
     o[1] = __builtin_amdgcn_s_memrealtime();
@@ -1312,12 +1324,12 @@ int persist_group(int dflt) {
 // Resident workgroups of a persistent kernel on the current device (cached per
 // kernel instantiation and device).
 template <class K>
-int resident_blocks(K kernel, int &blocks, int &dev_cached) {
+int resident_blocks(K kernel, int &blocks, int &dev_cached, int block = kBlock) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if (blocks == 0 || dev != dev_cached) {
     int per_cu = 0, cus = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     blocks = std::max(1, per_cu) * std::max(1, cus);
     dev_cached = dev;
@@ -1329,7 +1341,7 @@ int resident_blocks(K kernel, int &blocks, int &dev_cached) {
 // (1: 1x1, 2: 2x1, 4: 2x2) of n frames, the stream's head set; *grid = the
 // launch's workgroups (the resident ones, fewer for a small batch).
 int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t stream, PersistQ &q,
-               uint32_t &grid) {
+               uint32_t &grid, int block = kBlock) {
   uint32_t *heads = nullptr;
   if (const int rc = stream_queue(stream, &heads)) return rc;
   q.heads = heads;
@@ -1351,8 +1363,9 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   }();
   q.cpf = banded ? (q.per_frame + 7) / 8 : 0;
   q.nper = q.cpf * (uint32_t)n;
-  grid = std::min<uint32_t>((uint32_t)blocks, (q.items + 3) / 4);
-  q.waves = grid * (kBlock / 64);
+  const uint32_t wpb = (uint32_t)block / 64;  // waves per workgroup
+  grid = std::min<uint32_t>((uint32_t)blocks, (q.items + wpb - 1) / wpb);
+  q.waves = grid * wpb;
   q.stamps = (g_persist_stamps && (int64_t)q.waves <= g_persist_stamps_cap) ? g_persist_stamps : nullptr;
   return RT_OK;
 }
@@ -1361,11 +1374,11 @@ template <class S, int MAXD, bool GENERAL>
 int launch_persist_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatch &fb, int n, int group,
                      hipStream_t stream) {
   static int blocks = 0, dev_cached = -1;
-  if (const int rc = resident_blocks(render_persist_kernel<S, MAXD, GENERAL>, blocks, dev_cached)) return rc;
+  if (const int rc = resident_blocks(render_persist_kernel<S, MAXD, GENERAL>, blocks, dev_cached, kPBlock)) return rc;
   PersistQ q;
   uint32_t grid = 0;
-  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid)) return rc;
-  render_persist_kernel<S, MAXD, GENERAL><<<grid, kBlock, 0, stream>>>(sc, pl, fb, q);
+  if (const int rc = make_queue(fb, n, group, blocks, stream, q, grid, kPBlock)) return rc;
+  render_persist_kernel<S, MAXD, GENERAL><<<grid, kPBlock, 0, stream>>>(sc, pl, fb, q);
   return RT_OK;
 }
 
