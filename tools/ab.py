@@ -6,7 +6,8 @@ launch machinery, so numbers are comparable with the bench).
   python tools/ab.py split [workload ...]   per-rank compute of the row-split
                                             renderer: EVERY rank r of N renders
                                             its 8-row bands (AB_NS="2,4,8"); the
-                                            max over ranks bounds the N-GPU scaling
+                                            max over ranks bounds the N-GPU scaling;
+                                            AB_STREAMS: streams per rank, default 2
   python tools/ab.py modes [workload ...]   primary and default shading
 
 workload: a key of bench.WORKLOADS (bunny, grid, grid_shipped, octree,
@@ -67,7 +68,8 @@ def main():
             for n in (int(x) for x in os.environ.get("AB_NS", "2,4,8").split(",")):
                 per = []
                 for r in range(n):
-                    ms, kms = timed(sc, prm, W, H, 2, 8, _lib.Tile(8, r, n, 0))
+                    ms, kms = timed(sc, prm, W, H, int(os.environ.get("AB_STREAMS", "2")), 8,
+                                    _lib.Tile(8, r, n, 0))
                     per.append((ms, kms))
                     print(f"{name} N={n} rank {r}: {ms:.4f} ms/frame ({base / ms:.2f}x of N=1), "
                           f"{kms:.4f} ms/launch of 8", flush=True)
