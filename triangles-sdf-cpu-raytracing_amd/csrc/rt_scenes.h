@@ -679,11 +679,12 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
                 : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt));
   // Rays still traversing: at most kCoopRays per branch of the fast/exact
   // dispatch above (each branch suspends on its own lane count), so up to
-  // 2 * kCoopRays; they are finished kCoopRays at a time.
+  // 2 * kCoopRays; they are finished 8 at a time (one per 8-lane group; a
+  // threshold above 8 means several rounds).
   uint64_t U = __ballot(suspended);  // wave-uniform
   while (U != 0) {
-    uint64_t R = 0, rest = U;  // the lowest kCoopRays rays of U
-    for (int i = 0; i < kCoopRays && rest != 0; ++i) {
+    uint64_t R = 0, rest = U;  // the lowest 8 rays of U
+    for (int i = 0; i < 8 && rest != 0; ++i) {
       R |= rest & (~rest + 1ull);
       rest &= rest - 1ull;
     }
