@@ -61,6 +61,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import gc
 import json
 import os
 import statistics
@@ -244,12 +245,20 @@ def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=
         issue(j, [params[(k + i) % len(params)] for i in range(n)])
     timed = split_launches(warmup, steps, batch)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for j, (k, n) in enumerate(timed):
-        issue(j, params[k:k + n], evs[j])
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+    # no garbage-collector pass inside the timed region: a full collection of this
+    # process's heap (torch, numpy, ctypes) stalls the host thread that issues the
+    # launches for milliseconds, longer than the 20-frame run itself
+    gc.collect()
+    gc.disable()
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for j, (k, n) in enumerate(timed):
+            issue(j, params[k:k + n], evs[j])
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    finally:
+        gc.enable()
     launches = [(a.elapsed_time(b), n) for (a, b), (_, n) in zip(evs, timed)]
     jl, (kl, nl) = len(timed) - 1, timed[-1]
     return wall, launches, bufs[jl % inflight][nl - 1]
@@ -297,12 +306,17 @@ def run_distributed(scene, params, warmup, steps, a, W, H):
             raise SystemExit("row-split gather: assembled warm-up frame differs from a whole-frame render")
     dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rs.render(params[warmup:warmup + steps])
-    rs.host_issue_s = time.perf_counter() - t0  # host time to issue every launch and signal
-    rs.drain()
-    dist.barrier()
-    wall = time.perf_counter() - t0
+    gc.collect()
+    gc.disable()  # as in run_single
+    try:
+        t0 = time.perf_counter()
+        rs.render(params[warmup:warmup + steps])
+        rs.host_issue_s = time.perf_counter() - t0  # host time to issue every launch and signal
+        rs.drain()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+    finally:
+        gc.enable()
     # render-launch duration of this rank's bands: the same launches (a.group frames each,
     # a.streams streams) rendered locally, HIP events on each launch's stream
     n = min(steps, 64)
@@ -453,8 +467,10 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
     scene, off = WL.scene_for(src)
     scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
     prm = orbit_params(warmup + steps, W, H, mode)
-    wall, launches, _ = run_single(scene, prm, warmup, steps, W, H, inflight=streams, batch=group)
+    wall, launches, (lc, lt) = run_single(scene, prm, warmup, steps, W, H, inflight=streams, batch=group)
     ms_step = wall * 1e3 / steps
+    _, _, (c1, t1) = run_single(scene, prm[warmup + steps - 1:], 0, 1, W, H, inflight=1)  # as the headline's check
+    frame_ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
     algo, per_ray = work_model(scene, prm[warmup:], None, W, H)
     rl = roofline(algo, ms_step, scene.device_bytes(), pmc.get(key), pmc_err, group)
     one = one_stream_leg(scene, prm, warmup, steps, W, H, group, algo, rl["peak"], rl["peak_kind"]) \
@@ -463,7 +479,8 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
            "value": round(W * H * steps / wall / 1e6, 1), "ms_per_step": round(ms_step, 4),
            "frac": rl["frac"], "peak_kind": rl["peak_kind"],
            "dram_frac": rl.get("dram", {}).get("frac"), "valu_frac": rl.get("valu_frac"),
-           "lane_util": rl.get("lane_util"), "1stream_launch_ms": one["kernel_ms_per_launch"] if one else None}
+           "lane_util": rl.get("lane_util"), "1stream_launch_ms": one["kernel_ms_per_launch"] if one else None,
+           "frame_check": frame_ok}
     if mode == "default":
         rays = per_ray.get("rays", 1.0)
         out["traced_rays_per_px"] = rays
@@ -600,9 +617,18 @@ def main():
 
     latency = None
     tile = None
+    frame_ok = None
     if not use_dist:
-        wall, launches, _ = run_single(scene, params, a.warmup, a.steps, W, H, inflight=a.streams, batch=a.group)
+        wall, launches, (lc, lt) = run_single(scene, params, a.warmup, a.steps, W, H, inflight=a.streams,
+                                              batch=a.group)
         detail["headline_launch_ms"] = [round(ms, 5) for ms, _ in launches]
+        # the last timed frame (the persistent multi-frame kernel) must equal the
+        # same frame rendered alone by the one-frame kernel (render_kernel): both
+        # are bit-exact against the oracle in tests/, so a timed path that drops
+        # or alters work shows here
+        k = a.warmup + a.steps - 1
+        _, _, (c1, t1) = run_single(scene, params[k:k + 1], 0, 1, W, H, inflight=1)
+        frame_ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
         if a.streams * a.group > 1:  # one frame at a time (latency), reported beside
             nl = min(a.steps, 64)
             lwall, ll, _ = run_single(scene, params, min(a.warmup, 8), nl, W, H, inflight=1)
@@ -649,6 +675,8 @@ def main():
                    "frames_per_launch": a.group, "streams": a.streams},
         "roofline": rl,
     }
+    if frame_ok is not None:
+        out["frame_check"] = {"last_timed_frame_equals_one_frame_kernel": frame_ok}
     if latency is not None:
         out["frame_latency"] = latency
     if not use_dist and a.streams > 1:
