@@ -388,7 +388,7 @@ __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, c
   }
 }
 
-template <class S, int SLOTS, bool GENERAL, int DIAG>
+template <class S, int SLOTS, bool GENERAL, int DIAG, int BT = kBlock>
 __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
                                             unsigned long long *counters, uint32_t *stk) {
   typename CntSel<DIAG>::T cnt{};
@@ -402,8 +402,11 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
     by = tl / gridDim.x;
   }
   const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
-  render_pixels<S, SLOTS, GENERAL, DIAG>(sc, pl, fa, cnt, stk, bx * kTile + (wave & 1) * 8 + (lane & 7),
-                                         by * kTile + (wave >> 1) * 8 + (lane >> 3));
+  if constexpr (BT == 64)  // one 8x8 wave tile per workgroup
+    render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, (int)bx * 8 + (lane & 7), (int)by * 8 + (lane >> 3));
+  else
+    render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, bx * kTile + (wave & 1) * 8 + (lane & 7),
+                                               by * kTile + (wave >> 1) * 8 + (lane >> 3));
   if constexpr (DIAG == 0) {
     if (fa.cost) {  // this wave's duration; the tile keeps its slowest wave's
       const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
@@ -459,12 +462,27 @@ constexpr int min_waves() {
   return (DIAG != 0 || SLOTS > 7) ? 1 : GENERAL ? RT_GENERAL_WAVES : S::kMinWaves;
 }
 
+// Workgroup of the one-frame kernel (render_kernel, DIAG == 0): 64 = one 8x8
+// wave tile per workgroup (the cost-ordered schedule then orders 8x8 tiles),
+// 256 = 16x16 tiles of 4 waves (A/B switch). The counting and stamping
+// variants (DIAG 1, 2) keep 16x16 tiles.
+#ifndef RT_FRAME_BLOCK
+#define RT_FRAME_BLOCK 256
+#endif
+constexpr int kFBlock = RT_FRAME_BLOCK;
+constexpr int kFTile = kFBlock == 64 ? 8 : kTile;
+static_assert(kFBlock == 64 || kFBlock == kBlock, "one-frame workgroup: one wave or the 16x16 tile");
+template <int DIAG>
+constexpr int frame_block() { return DIAG == 0 ? kFBlock : kBlock; }
+template <int DIAG>
+constexpr int frame_tile() { return DIAG == 0 ? kFTile : kTile; }
+
 template <class S, int SLOTS, bool GENERAL, int DIAG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, DIAG>())))
+__global__ __launch_bounds__(frame_block<DIAG>()) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, DIAG>())))
 void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
-  __shared__ uint32_t stk[SLOTS * S::kFields * kBlock];
-  render_body<S, SLOTS, GENERAL, DIAG>(sc, pl, fa, counters, stk);
+  __shared__ uint32_t stk[SLOTS * S::kFields * frame_block<DIAG>()];
+  render_body<S, SLOTS, GENERAL, DIAG, frame_block<DIAG>()>(sc, pl, fa, counters, stk);
 }
 
 // Several frames in one launch: blockIdx.z selects the frame. The tiles of
@@ -1150,6 +1168,7 @@ template <class S, int MAXD>
 void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool general,
                      hipStream_t stream, unsigned long long *counters, int diag) {
   const dim3 grid((fa.W + kTile - 1) / kTile, (fa.rows_local + kTile - 1) / kTile);
+  const dim3 fgrid((fa.W + kFTile - 1) / kFTile, (fa.rows_local + kFTile - 1) / kFTile);
   if (diag == 1) {
     if (general)
       render_kernel<S, MAXD, true, 1><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
@@ -1162,9 +1181,9 @@ void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool 
       render_kernel<S, MAXD, false, 2><<<grid, kBlock, 0, stream>>>(sc, pl, fa, counters);
   } else {
     if (general)
-      render_kernel<S, MAXD, true, 0><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+      render_kernel<S, MAXD, true, 0><<<fgrid, kFBlock, 0, stream>>>(sc, pl, fa, nullptr);
     else
-      render_kernel<S, MAXD, false, 0><<<grid, kBlock, 0, stream>>>(sc, pl, fa, nullptr);
+      render_kernel<S, MAXD, false, 0><<<fgrid, kFBlock, 0, stream>>>(sc, pl, fa, nullptr);
   }
 }
 
@@ -1219,7 +1238,7 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
                   unsigned long long *counters = nullptr, int diag = 0) {
   FrameArgs fa = fa_in;
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
-  const uint32_t gx = (fa.W + kTile - 1) / kTile, gy = (fa.rows_local + kTile - 1) / kTile;
+  const uint32_t gx = (fa.W + kFTile - 1) / kFTile, gy = (fa.rows_local + kFTile - 1) / kFTile;
   fa.order = nullptr;
   fa.cost = nullptr;
   if (diag == 0) {
