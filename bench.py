@@ -264,6 +264,12 @@ def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=
     return wall, launches, bufs[jl % inflight][nl - 1]
 
 
+def verify_frames(a, warmup):
+    """N>1 warm-up = verification pass: enough frames to reuse every slot group
+    at least twice and end on a partial group."""
+    return max(warmup, 2 * a.group * a.depth + a.group // 2 + 1, a.group * a.streams * a.depth)
+
+
 def per_frame_ms(launches):
     """Frame-weighted kernel time per frame over the timed launches."""
     return sum(ms for ms, _ in launches) / sum(n for _, n in launches)
@@ -279,31 +285,48 @@ def run_distributed(scene, params, warmup, steps, a, W, H):
     gathers are host-synchronous."""
     from rtamd.rowsplit import RowSplitRenderer
 
-    def make(exchange):
-        r = RowSplitRenderer(scene, W, H, band_rows=a.band_rows, group=a.group, depth=a.depth,
-                             streams=a.streams, exchange=exchange)
-        # warm every stream and slot group the timed region will use
-        r.render(params[:max(warmup, a.group * a.streams * a.depth)])
-        r.drain()
-        return r
+    nverify = verify_frames(a, warmup)
 
-    rs = make(a.exchange)
-    # the warm-up's last assembled frame must equal a whole-frame render on rank 0;
-    # a p2p exchange that fails this (IPC mapping, peer-store visibility) is replaced
-    # by the RCCL gather before anything is timed
-    ok = 1
-    nw = max(warmup, a.group * a.streams * a.depth)
-    if dist.get_rank() == 0:
-        _, _, (c1, t1) = run_single(scene, params[nw - 1:nw], 0, 1, W, H, inflight=1)
-        fc, ft = rs.last()
-        ok = int(torch.equal(c1, fc) and torch.equal(t1.view(torch.int32), ft.view(torch.int32)))
-    if not rs._all_ok(ok):
+    def make(exchange):
+        """A renderer whose warm-up is a verification pass: nverify frames (every
+        slot group reused at least twice, ending on a partial group) go through
+        the slot / signal protocol and rank 0 keeps a copy of EVERY assembled
+        frame (on_frame, in stream order before the slot is cleared), each then
+        compared bitwise with the same frame rendered whole by the one-frame
+        kernel. -> (renderer, ok on every rank, frames that differed on rank 0)"""
+        got = {}
+
+        def keep(k, c, t):
+            got[k] = (c.clone(), t.clone())
+        r = RowSplitRenderer(scene, W, H, band_rows=a.band_rows, group=a.group, depth=a.depth,
+                             streams=a.streams, exchange=exchange, on_frame=keep)
+        r.render(params[:nverify])
+        r.drain()
+        r.on_frame = None
+        bad = []
+        if dist.get_rank() == 0:
+            for k in range(nverify):
+                _, _, (c1, t1) = run_single(scene, params[k:k + 1], 0, 1, W, H, inflight=1)
+                fc, ft = got.get(k, (None, None))
+                if fc is None or not (torch.equal(c1, fc) and torch.equal(t1.view(torch.int32),
+                                                                          ft.view(torch.int32))):
+                    bad.append(k)
+        got.clear()
+        return r, r._all_ok(int(not bad)), bad
+
+    # a p2p exchange that fails the check (IPC mapping, peer-store visibility) is
+    # replaced by the RCCL gather before anything is timed
+    rs, ok, bad = make(a.exchange)
+    rs.verified = {"frames": nverify, "exchange": rs.exchange, "differing": bad}
+    if not ok:
         if rs.exchange == "p2p":
             rs.close()
-            rs = make("gather")
-            rs.fallback = "p2p warm-up frame differed from a whole-frame render"
-        else:
-            raise SystemExit("row-split gather: assembled warm-up frame differs from a whole-frame render")
+            rs, ok, bad2 = make("gather")
+            rs.verified = {"frames": nverify, "exchange": rs.exchange, "differing": bad2,
+                           "p2p_differing": bad}
+            rs.fallback = f"p2p: {len(bad)} of {nverify} assembled frames differed from whole-frame renders"
+        if not ok:
+            raise SystemExit("row-split gather: assembled frames differ from whole-frame renders")
     dist.barrier()
     torch.cuda.synchronize()
     gc.collect()
@@ -330,13 +353,17 @@ L2_TOTAL_BYTES = 8 * 4 << 20  # 8 XCDs x 4 MiB
 
 
 def peak_for(achieved, scene_bytes):
-    """The roof the algorithmic bytes are held against. A scene that fits the
-    aggregate L2 (32 MiB) is served from the caches by construction, and so is
-    any rate above the 8 TB/s HBM peak: the L2 roof. Only a larger scene read
-    below the HBM rate (the 64 MiB 256^3 grid) is held against HBM. Deciding
-    by residency, not by the rate alone, keeps a workload on one roof from run
-    to run (the 65^3 grid sits near 8 TB/s and would otherwise switch roofs,
-    and its fraction by ~4x, with a few percent of run-to-run noise)."""
+    """The roof the algorithmic bytes are held against. Residency decides
+    first: a scene that fits the aggregate L2 (32 MiB) is served from the
+    caches by construction, so it is held against the L2 roof whatever its
+    rate (the 65^3 grid sits near 8 TB/s and would otherwise switch roofs, and
+    its fraction by ~4x, on a few percent of run-to-run noise). A larger scene
+    (the 64 MiB 256^3 grid, the ~60 MB 1.1 M-triangle mesh) is held against
+    HBM, except when its algorithmic bytes arrive faster than HBM can deliver
+    at all (the 1.1 M-triangle mesh at ~12 TB/s): those bytes are cache-served
+    too, and an HBM fraction above 1 would name no roof. Such a workload could
+    change roofs if its rate drifted across 8 TB/s, so the line carries both
+    fractions (hbm_frac_of_algorithmic, l2_frac_of_algorithmic)."""
     if scene_bytes <= L2_TOTAL_BYTES or achieved > HBM_PEAK_GBS:
         return L2_PEAK_GBS, "l2"
     return HBM_PEAK_GBS, "hbm"
@@ -361,11 +388,12 @@ def roofline(algo_frame, ms_step, scene_bytes, ctr=None, pmc_err=None, group=8):
     dur = ms_step * 1e-3
     achieved = algo_frame / dur / 1e9
     peak, kind = peak_for(achieved, scene_bytes)
-    rl = {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "peak_kind": kind, "unit": "GB/s",
+    rl = {"bound": kind, "achieved": round(achieved, 1), "peak": peak, "peak_kind": kind, "unit": "GB/s",
           "frac": round(achieved / peak, 4), "traffic": None, "per": "frame (step); time = ms_per_step",
           "algorithmic_bytes_per_frame": int(algo_frame), "ms_per_step": round(ms_step, 5),
           "scene_device_bytes": int(scene_bytes),
-          "hbm_frac_of_algorithmic": round(achieved / HBM_PEAK_GBS, 4)}
+          "hbm_frac_of_algorithmic": round(achieved / HBM_PEAK_GBS, 4),
+          "l2_frac_of_algorithmic": round(achieved / L2_PEAK_GBS, 4)}
     if pmc_err or not ctr or "FETCH_SIZE" not in ctr or "SQ_INSTS_VALU" not in ctr:
         rl["pmc_error"] = (pmc_err or "no counters")[:160]
         return rl
@@ -494,9 +522,12 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
 
 def drop_in(scene, params, W, H, frames=16):
     """rt_render on HOST buffers (Renderer::draw's surface, INTEGRATION.md):
-    ms per frame including the copies, cleared frames (the app's
-    frameBuf.clear() + draw -> RT_FLAG_CLEAR: no upload) and tPrev frames
-    (upload of color and t, then write-on-hit), on pageable and pinned buffers."""
+    ms per frame including the copies, on pageable and pinned buffers, for
+    three ways of calling it: `clear` (RT_FLAG_CLEAR: clear + draw fused, no
+    upload, the whole frame copied back), `cleared` (RT_FLAG_CLEAR |
+    RT_FLAG_HITS_ONLY: the app's frameBuf.clear() + draw, main.cpp:197-203; no
+    upload, only the hits' bounding box copied back) and `tprev` (no flag:
+    upload of color and t, write-on-hit, the hits' box copied back)."""
     import numpy as np
     L = rtamd.lib()
     out = {}
@@ -507,12 +538,18 @@ def drop_in(scene, params, W, H, frames=16):
             rtamd._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
             rtamd._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
         try:
-            for clear in (True, False):
-                scene.render(params[0], c, t, clear=clear)  # warm
-                t0 = time.perf_counter()
-                ks = [scene.render(params[k % len(params)], c, t, clear=clear) for k in range(frames)]
-                wall = (time.perf_counter() - t0) * 1e3 / frames
-                out[f"{'pinned' if pinned else 'pageable'}_{'clear' if clear else 'tprev'}_ms"] = round(wall, 4)
+            for how in ("clear", "cleared", "tprev"):
+                kw = {"clear": how == "clear", "cleared": how == "cleared"}
+                scene.render(params[0], c, t, **kw)  # warm
+                wall, ks = 0.0, []
+                for k in range(frames):
+                    if how == "cleared":  # the app's frameBuf.clear(), outside the timed call
+                        c.fill(0)
+                        t.fill(np.inf)
+                    t0 = time.perf_counter()
+                    ks.append(scene.render(params[k % len(params)], c, t, **kw))
+                    wall += time.perf_counter() - t0
+                out[f"{'pinned' if pinned else 'pageable'}_{how}_ms"] = round(wall * 1e3 / frames, 4)
                 out.setdefault("kernel_ms", round(statistics.median(ks), 4))
         finally:
             if pinned:
@@ -572,6 +609,82 @@ def cpu_baseline(entry, budget_s, max_frames):
             "sample": f"{frames} orbit frames, {src} {W}x{H} {mode}"}, why
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, json_out, grace_s=60.0, cmd=None, ndev=None):
+    """`--gpus N` (N > 1) run without a launcher: start N rank processes of this
+    same command, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+    environment, rendezvous on 127.0.0.1), as torch.distributed.run would. This
+    process never touches the GPU (torch.cuda.device_count() does not initialise
+    it), so nothing is exec'd from a GPU-initialised process. Rank 0's JSON line
+    is relayed to stdout; the exit code is the worst rank's. When one rank fails
+    the others get `grace_s` to finish before their process groups are killed
+    (a rank blocked in a collective with a dead peer would wait forever).
+    `cmd` / `ndev` replace this command and the device count (tests).
+    Returns the exit code."""
+    import signal
+    import subprocess
+    import threading
+    backend = os.environ.get("RTAMD_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count() if ndev is None else ndev
+    if ndev < 1:
+        print("bench.py: --gpus needs a HIP device (the renderer has no CPU path)", file=sys.stderr)
+        return 2
+    if backend == "nccl" and ndev < n:
+        print(f"bench.py: --gpus {n} but {ndev} HIP device(s) visible; refusing to report an {n}-GPU line "
+              f"(RTAMD_DIST_BACKEND=gloo shares the devices between ranks as a protocol test)", file=sys.stderr)
+        return 2
+    port = _free_port()
+    cmd = cmd or [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), RANK=str(r),
+                   LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                      start_new_session=True))
+    lines = []
+
+    def relay():  # rank 0's stdout: the JSON line to ours, anything else to stderr
+        for raw in procs[0].stdout:
+            s = raw.decode(errors="replace")
+            if s.startswith("{"):
+                lines.append(s.strip())
+            else:
+                sys.stderr.write(s)
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    print(f"bench.py: killing rank {procs.index(p)} (a peer failed {grace_s:.0f} s ago)",
+                          file=sys.stderr)
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    th.join(timeout=10)
+    rcs = [p.wait() for p in procs]
+    rc = max((abs(x) for x in rcs), default=0)
+    if rc == 0 and not lines:
+        print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
+        rc = 1
+    if rc == 0:
+        print(lines[-1], file=json_out, flush=True)
+    else:
+        print(f"bench.py: rank exit codes {rcs}; no line reported", file=sys.stderr)
+    return rc
+
+
 def main():
     # libraries (RCCL, gloo) print banners to stdout: send fd 1 to stderr and
     # keep the real stdout for the one JSON line
@@ -580,13 +693,18 @@ def main():
     a = parse()
     if not 1 <= a.group <= 8:
         raise SystemExit("--group must be 1..8 (frames per launch)")
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
     key, entry = workload_entry(a.workload)
     src, W, H, mode, cfg, desc = entry
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus, json_out))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+        # never report a line for a GPU count other than the one asked for
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}")
     use_dist = world > 1 or a.dist
     pmc, pmc_err = {}, "skipped (--no-pmc or N>1)"
     if not use_dist and not a.no_pmc:
@@ -596,6 +714,8 @@ def main():
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
+    if use_dist and world > ndev and os.environ.get("RTAMD_DIST_BACKEND", "nccl") == "nccl":
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} HIP device(s); RCCL needs one GPU per rank")
     device = local % ndev  # ranks > devices only for the gloo protocol test
     torch.cuda.set_device(device)
     if use_dist:
@@ -612,7 +732,7 @@ def main():
 
     scene, off = WL.scene_for(src)
     scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
-    params = orbit_params(max(a.warmup + a.steps, a.group * a.streams * a.depth), W, H, mode)
+    params = orbit_params(max(a.warmup + a.steps, verify_frames(a, a.warmup)), W, H, mode)
     detail = {"cmd": " ".join(sys.argv), "headline": key}
 
     latency = None
@@ -685,7 +805,12 @@ def main():
     if use_dist:
         out["rank_kernel_ms_per_frame"] = {"per_rank": rank_kms, "max": max(rank_kms)}
     if use_dist and rank == 0:
-        out["frame_check"] = {"assembled_equals_single_render": check_equal,
+        v = rs.verified
+        out["frame_check"] = {"assembled_equals_single_render": check_equal and not v["differing"],
+                              "last_timed_frame": check_equal,
+                              "verify_pass": {"frames_checked": v["frames"], "differing": v["differing"][:16],
+                                              **({"p2p_differing": v["p2p_differing"][:16]}
+                                                 if "p2p_differing" in v else {})},
                               "backend": dist.get_backend(), "exchange": rs.exchange,
                               "fallback": getattr(rs, "fallback", None)}
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)

@@ -49,9 +49,11 @@ enum rt_scene_kind { RT_SCENE_MESH = 1, RT_SCENE_GRID = 2, RT_SCENE_OCTREE = 3 }
 #define RT_FLAG_TILE_NATURAL 2u /* with a tile: write this rank's bands at their own rows of a
                                    full W*H frame (e.g. rank 0's frame mapped over xGMI by
                                    rt_ipc_open) instead of packed */
-#define RT_FLAG_HITS_ONLY 4u /* with RT_FLAG_CLEAR: the frame is already cleared (rt_clear_device),
-                                so only hit pixels are stored -- the same image as CLEAR alone,
-                                with misses costing no stores (no xGMI traffic for background) */
+#define RT_FLAG_HITS_ONLY 4u /* with RT_FLAG_CLEAR: the frame is already cleared (rt_clear_device,
+                                or FrameBuffer::clear() for rt_render's host buffers), so only hit
+                                pixels are stored -- the same image as CLEAR alone, with misses
+                                costing no stores (no xGMI traffic for background; for rt_render,
+                                only the hits' bounding box is copied back) */
 
 typedef struct rt_scene rt_scene; /* opaque: owns the device copy of one scene on one GPU */
 typedef struct rt_sdf_mesh rt_sdf_mesh; /* opaque: a triangle mesh prepared for SDF queries */
@@ -87,6 +89,10 @@ typedef struct rt_tile {
 /* ---- errors / device ---------------------------------------------------- */
 const char *rt_last_error(void);
 int rt_abi_version(void);
+/* First 16 hex digits of the sha256 of the sources this library was built
+ * from (triangles-sdf-cpu-raytracing_amd/csrc/{*.cpp,*.h,*.hip} sorted, then
+ * include/rtamd.h): ties a shipped binary to a source tree. */
+const char *rt_build_id(void);
 /* Number of visible HIP devices (0 if none); never fails. */
 int rt_device_count(void);
 /* Select the HIP device used by subsequent scene creation on this thread. */
@@ -150,6 +156,13 @@ int rt_scene_destroy(rt_scene *s);
 /* ---- frames ------------------------------------------------------------- */
 /* Renderer::draw on HOST buffers color[W*H] (RGBA8 packed, R in the low byte)
  * and t[W*H] (row-major y*W+x). Uploads, renders, downloads, synchronises.
+ * flags: 0 (t read as tPrev, write on hit), RT_FLAG_CLEAR (clear + draw, every
+ * pixel written) or RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY (the caller's buffers
+ * already hold a cleared frame, src/main.cpp:197). Without RT_FLAG_CLEAR, or
+ * with both, only the bounding box of the stored hits is copied back: the
+ * other pixels keep the caller's values, as Renderer::draw leaves them. Once a
+ * copy is queued every return, an error included, waits for it first, so the
+ * buffers may be unpinned / freed when the call returns.
  * *ms (optional) receives the kernel time in milliseconds (HIP events). */
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W,
               int32_t H, uint32_t flags, float *ms);

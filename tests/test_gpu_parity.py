@@ -207,6 +207,8 @@ def test_no_fallback_library_loaded(gpu):
     want = os.path.basename(os.environ.get("RTAMD_LIB") or "librtamd.so")
     assert rtamd.lib()._name.endswith(want)
     assert rtamd.device_count() >= 1
+    if not os.environ.get("RTAMD_LIB"):  # the shipped binary was built from this tree's sources
+        assert rtamd.lib().rt_build_id().decode() == rtamd._lib.source_build_id()
 
 
 def test_golden_fixture_frames(gpu):

@@ -34,6 +34,14 @@ def test_library_exports_every_header_symbol(rt):
     assert rt.lib().rt_abi_version() == 6
 
 
+def test_library_build_id_matches_tree(rt):
+    """librtamd.so (the binary the GPU box runs) was built from this tree's
+    sources: rt_build_id() equals the hash of csrc/ + include/rtamd.h."""
+    if os.environ.get("RTAMD_LIB"):
+        pytest.skip("a variant library injected through RTAMD_LIB")
+    assert rt.lib().rt_build_id().decode() == rt._lib.source_build_id()
+
+
 @pytest.mark.parametrize("name", ["cube.obj", "spot.obj", "stanford-bunny.obj"])
 def test_obj_loader_matches_oracle(rt, ref, name):
     p = rt.data.path(name)

@@ -215,6 +215,79 @@ def test_drop_in_render_host_buffers(gpu):
                 L.rt_host_unpin(t.ctypes.data)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_drop_in_partial_download(gpu, pinned):
+    """rt_render copies back only the bounding box of the stored hits when the
+    caller's buffers hold a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY)
+    or a tPrev frame (no flag): every other pixel keeps the caller's value,
+    exactly as Renderer::draw over the same buffers leaves it. Narrow boxes go
+    as 2-D copies, wide ones as whole rows, no hit copies nothing."""
+    rt = gpu
+    L = rt.lib()
+    name, W, H = "stanford-bunny.obj", 320, 180
+    sc = S.gpu_scene(name)
+    S.set_planes(name, "primary", sc)
+    rs = S.ref_scene(name)
+    S.set_planes(name, "primary", rs)
+    c = np.zeros((H, W), np.uint32)
+    t = np.full((H, W), np.inf, np.float32)
+    if pinned:
+        rt._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+        rt._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+    try:
+        # far camera: narrow box (2-D copy); near: wide (rows); away: no hit
+        for pos in ((0.0, 0.1, 3.5), (0.2, 0.1, 0.9), (0.0, 0.0, -30.0)):
+            c[:] = 0
+            t[:] = np.inf
+            sc.render(S.params(name, W, H, "primary", pos, "gpu"), c, t, cleared=True)
+            rc, rt_, _, _ = rs.render(S.params(name, W, H, "primary", pos, "ref"), W, H)
+            assert np.array_equal(c, rc) and np.array_equal(t.view(np.uint32), rt_.view(np.uint32)), pos
+        # tPrev over a frame holding other values everywhere (a sentinel region included)
+        c[:] = 0x11223344
+        t[:] = 1.5
+        t[:40, :60] = np.inf
+        rc, rt_ = c.copy(), t.copy()
+        pos = (0.6, 0.2, 2.2)
+        sc.render(S.params(name, W, H, "primary", pos, "gpu"), c, t, clear=False)
+        rs.render(S.params(name, W, H, "primary", pos, "ref"), W, H, color=rc, t=rt_)
+        assert np.array_equal(c, rc) and np.array_equal(t.view(np.uint32), rt_.view(np.uint32))
+    finally:
+        if pinned:
+            L.rt_host_unpin(c.ctypes.data)
+            L.rt_host_unpin(t.ctypes.data)
+
+
+def test_drop_in_failure_leaves_no_copy_in_flight(gpu):
+    """An rt_render that fails after queueing its uploads (injected) returns
+    only once its copy streams are idle, so pinned buffers can be unpinned and
+    freed at once; the next call renders normally."""
+    import ctypes as C
+    rt = gpu
+    L = rt.lib()
+    L.rtx_render_inject_failure.argtypes = [C.c_int32]
+    L.rtx_render_streams_idle.argtypes = [C.c_void_p]
+    name, W, H = "stanford-bunny.obj", 1920, 1080
+    sc = S.gpu_scene(name)
+    S.set_planes(name, "primary", sc)
+    c = np.zeros((H, W), np.uint32)
+    t = np.full((H, W), np.inf, np.float32)
+    rt._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+    rt._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+    P = S.params(name, W, H, "primary", (0.0, 0.0, 2.5), "gpu")
+    try:
+        L.rtx_render_inject_failure(1)
+        with pytest.raises(rt.RtError, match="injected"):
+            sc.render(P, c, t, clear=False)  # tPrev: both uploads queued before the failure
+        assert L.rtx_render_streams_idle(sc._h) == 1
+    finally:
+        L.rtx_render_inject_failure(0)
+        L.rt_host_unpin(c.ctypes.data)
+        L.rt_host_unpin(t.ctypes.data)
+    sc.render(P, c, t, clear=True)
+    rc, rt_ = S.ref_frame(name, W, H, "primary")
+    assert np.array_equal(c, rc)
+
+
 def test_hits_only_needs_clear(gpu):
     from rtamd import _lib
     sc = S.gpu_scene("cube.obj")

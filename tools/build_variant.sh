@@ -26,4 +26,4 @@ else
   /opt/rocm/bin/hipcc $HIPF $2 -c -o build/var/rt_device_$1.o $SRC
   DEV=build/var/rt_device_$1.o BVH=build/rt_bvhgpu.o
 fi
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/var_$1.so build/rt_host.o build/rt_bvhstage.o build/rt_meshops.o $DEV build/rt_sdfgen.o $BVH -lgomp
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/var_$1.so build/rt_host.o build/rt_bvhstage.o build/rt_meshops.o $DEV build/rt_sdfgen.o $BVH build/rt_buildid.o -lgomp

@@ -3,7 +3,12 @@
 # a rocprofv3 kernel-stats pass and A/B legs. usage (on the box):
 #   tools/gpu_session.sh OUT step [step ...]
 # steps:
-#   tests | fulltests | smoke | bench | bench128 | prof | split | split_large | dist_gloo | dist_rccl1
+#   tests | fulltests | smoke | bench | bench128 | prof | prof_driver | split | split_large
+#   dist_gloo          bench.py --gpus 2 as the driver would run it without a launcher
+#                      (it spawns its 2 ranks; gloo, both on the one GPU)
+#   dist_gloo_run      the same through torch.distributed.run
+#   dist_rccl1         RCCL at world size 1 through the distributed path (--dist)
+#   bvh                GPU BVH builder tests + build timing (tools/bvh_time.py)
 #   benchw=KEY         bench.py --workload KEY (20 steps, headline only)
 #   ab=VAR=a,VAR2=b    tools/ab.py batch on $AB_WL (default bunny) under those
 #                      settings (RTAMD_LIB=<lib/var_x.so> selects a build variant,
@@ -44,7 +49,11 @@ for step in "$@"; do
     split_large) run split_large 600 python tools/ab.py split mesh_large || exit 1 ;;
     benchw=*) run "bench_$arg" 600 python bench.py --workload "$arg" --steps 20 --warmup 5 --no-extra \
                 --no-cpu-baseline --detail "$OUT/bench_${arg}_detail.json" && grep "^{" "$OUT/bench_$arg.log" | tail -n 1 > "$OUT/bench_$arg.json" || exit 1 ;;
-    dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && grep "^{" "$OUT/dist_gloo.log" | tail -n 1 > "$OUT/dist_gloo.json" || exit 1 ;;
+    dist_gloo) run dist_gloo 600 env RTAMD_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 \
+                 --detail "$OUT/dist_gloo_detail.json" && grep "^{" "$OUT/dist_gloo.log" | tail -n 1 > "$OUT/dist_gloo.json" || exit 1 ;;
+    bvh) run bvhtests 400 python -u -m pytest tests/test_bvhgpu.py -x -q --timeout 300 --timeout-method thread || exit 1
+         run bvh_time 300 env RTAMD_BVH_TIMING=1 OMP_NUM_THREADS=16 python tools/bvh_time.py || exit 1 ;;
+    dist_gloo_run) run dist_gloo_run 600 env RTAMD_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 && grep "^{" "$OUT/dist_gloo_run.log" | tail -n 1 > "$OUT/dist_gloo_run.json" || exit 1 ;;
     dist_rccl1) run dist_rccl1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 20 --warmup 5 --dist && grep "^{" "$OUT/dist_rccl1.log" | tail -n 1 > "$OUT/dist_rccl1.json" || exit 1 ;;
     ab=*) echo "== $tag [$arg]"; run "$tag" 300 env "${envs[@]}" python tools/ab.py batch ${AB_WL:-bunny} || exit 1
           grep -v amdgpu "$OUT/$tag.log" ;;

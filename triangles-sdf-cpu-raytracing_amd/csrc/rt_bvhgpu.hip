@@ -990,7 +990,7 @@ struct Sorter {
     }
     uint32_t m = (uint32_t)act.size(), E = 0;
     for (const Seg &s : act) E += s.last - s.first;
-    if (m > segcap || ser.size() > serial.cap) return rterr::set(RT_E_DEVICE, "sort: segment list bound");
+    if (m > segcap || ser.size() > serial.cap) return rterr::set(RT_E_DEVICE, "bound: sort segment list");
     uint32_t hc[kCtlWords] = {};
     hc[0] = (uint32_t)ser.size();
     hc[4] = m;
@@ -1007,7 +1007,7 @@ struct Sorter {
     uint32_t mb = m, Eb = E;
     while (mb > 0) {
       for (int b = 0; b < batch && mb > 0; ++b, ++r) {
-        if (r >= kMaxRounds) return rterr::set(RT_E_DEVICE, "sort: partition round bound");
+        if (r >= kMaxRounds) return rterr::set(RT_E_DEVICE, "bound: sort partition rounds");
         ++pt->rounds;
         const Round R{(r & 1) ? segB.p : segA.p, (r & 1) ? segA.p : segB.p, ctl.p, r};
         const uint32_t gm = (mb + kRoundT - 1) / kRoundT, gt = (Eb + kRoundTile - 1) / kRoundTile,
@@ -1052,9 +1052,14 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
                     std::string &err, unsigned want) {
   // every device-side failure is reported as "GPU BVH build: <step>: <HIP
   // error>" (RT_E_DEVICE at the C ABI; in AUTO mode the host builder takes
-  // over); input errors carry no prefix (RT_E_INVALID)
+  // over unless the fault is sticky); a bound of the builder's own stage logic
+  // that is exceeded is "GPU BVH builder bound: <what>" (RT_E_DEVICE, never
+  // hidden by the fallback: it is a builder bug, not a device failure); input
+  // errors carry no prefix (RT_E_INVALID)
   auto fail = [&](const char *what) {
-    err = std::string("GPU BVH build: ") + what + ": " + rterr::get();
+    const std::string m = rterr::get();
+    err = m.rfind("bound: ", 0) == 0 ? "GPU BVH builder bound: " + std::string(what) + ": " + m.substr(7)
+                                     : std::string("GPU BVH build: ") + what + ": " + m;
     return false;
   };
   auto hfail = [&](const char *what, hipError_t e) {
@@ -1207,7 +1212,10 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     }
     // createNode's FIFO, candidate by candidate (triangles_raytracing.cpp:162-173)
     std::string ferr;
-    if (!SG.fifo(ferr)) return hfail(ferr.c_str(), hipErrorInvalidValue);
+    if (!SG.fifo(ferr)) {
+      err = "GPU BVH builder bound: createNode FIFO: " + ferr;
+      return false;
+    }
     pt.hstop(1);
     pt.hstart();
     if (T) {

@@ -64,6 +64,10 @@ struct FrameArgs {
   int32_t band_rows, rank, nranks, rows_local;
   const uint32_t *order;  // block -> tile schedule (NULL: blockIdx order)
   uint32_t *cost;         // per-tile cost of this frame (shader cycles, max over waves), or NULL
+  // one-frame kernel: bounding box of the pixels a hit was stored to, as
+  // (min x, -max x, min y, -max y) in buffer coordinates (four atomicMin
+  // words, initialised to INT32_MAX), or NULL (rt_render's partial download)
+  int32_t *hit_box;
 };
 
 // ---------------------------------------------------------- scene adapters --
@@ -284,10 +288,22 @@ __device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
-#ifdef RT_PLAIN_FB_STORES
-  *p = v;
-#else
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Peer frames (RT_FLAG_TILE_NATURAL, the row-split p2p exchange): a system-
+// scope release after the wave's last peer store. The stores above are relaxed;
+// the fence waits for them to complete and makes them visible at system scope
+// before the wave ends, so the RCCL completion signal the host enqueues after
+// this kernel on the same stream cannot overtake them over xGMI, whatever the
+// end-of-kernel release of the dispatch covers. Once per wave (A/B switch
+// RT_PEER_RELEASE=0 drops it).
+#ifndef RT_PEER_RELEASE
+#define RT_PEER_RELEASE 1
+#endif
+__device__ __forceinline__ void peer_release(uint32_t flags) {
+#if RT_PEER_RELEASE
+  if (flags & RT_FLAG_TILE_NATURAL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 #endif
 }
 
@@ -332,13 +348,15 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 // 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
 
 // One pixel per lane of the wave's 8x8 tile: column xo, rank-local row yl.
+// Returns true iff this lane stored a hit (its pixel differs from a cleared
+// frame's or from tPrev).
 template <class S, int SLOTS, bool GENERAL, int DIAG, int B = kBlock, class CT>
-__device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
+__device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
                                               CT &cnt, uint32_t *stk, int xo, int yl) {
   const bool active = xo < fa.W && yl < fa.rows_local;
   // wave-cooperative primary path: every lane of the wave takes part
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
-  if (DIAG == 0 && !kWaveCoop && !active) return;
+  if (DIAG == 0 && !kWaveCoop && !active) return false;
   if (active || kWaveCoop) {  // (the counting variant keeps every lane for its wave reduction)
     LdsStack<B, S::kFields> st{stk + threadIdx.x};
     const int yo = image_row(active ? yl : 0, fa);
@@ -385,7 +403,9 @@ __device__ __forceinline__ void render_pixels(const S &sc, const PlaneDev &pl, c
       fb_store(fa.color + idx, pack_rgba(c), peer);
       fb_store(fa.t + idx, t, peer);
     }
+    return active && store;
   }
+  return false;
 }
 
 template <class S, int SLOTS, bool GENERAL, int DIAG, int BT = kBlock>
@@ -402,11 +422,25 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
     by = tl / gridDim.x;
   }
   const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
-  if constexpr (BT == 64)  // one 8x8 wave tile per workgroup
-    render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, (int)bx * 8 + (lane & 7), (int)by * 8 + (lane >> 3));
-  else
-    render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, bx * kTile + (wave & 1) * 8 + (lane & 7),
-                                               by * kTile + (wave >> 1) * 8 + (lane >> 3));
+  const int xo = BT == 64 ? (int)bx * 8 + (lane & 7) : (int)bx * kTile + (wave & 1) * 8 + (lane & 7);
+  const int yl = BT == 64 ? (int)by * 8 + (lane >> 3) : (int)by * kTile + (wave >> 1) * 8 + (lane >> 3);
+  const bool stored = render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, xo, yl);
+  if constexpr (DIAG == 0) {
+    if (fa.hit_box && __ballot(stored)) {  // this wave's stored pixels into the frame's hit box
+      int32_t v[4] = {stored ? xo : INT32_MAX, stored ? -xo : INT32_MAX, stored ? yl : INT32_MAX,
+                      stored ? -yl : INT32_MAX};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const int32_t o = __shfl_xor(v[i], off, 64);
+          v[i] = o < v[i] ? o : v[i];
+        }
+      if (lane == __ffsll((unsigned long long)__ballot(1)) - 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicMin(fa.hit_box + i, v[i]);
+    }
+  }
   if constexpr (DIAG == 0) {
     if (fa.cost) {  // this wave's duration; the tile keeps its slowest wave's
       const uint64_t dt = __builtin_amdgcn_s_memtime() - c0;
@@ -483,6 +517,7 @@ void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
   __shared__ uint32_t stk[SLOTS * S::kFields * frame_block<DIAG>()];
   render_body<S, SLOTS, GENERAL, DIAG, frame_block<DIAG>()>(sc, pl, fa, counters, stk);
+  peer_release(fa.flags);
 }
 
 // Several frames in one launch: blockIdx.z selects the frame. The tiles of
@@ -525,6 +560,7 @@ void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
     render_pixels<S, SLOTS, GENERAL, 0, kBBlock>(sc, pl, fb.f[blockIdx.z], cnt, stk, (int)blockIdx.x * 8 + (lane & 7),
                                                  (int)blockIdx.y * 8 + (lane >> 3));
   }
+  peer_release(fb.f[0].flags);
 }
 
 // Persistent form of render_batch_kernel: a grid of just the resident blocks;
@@ -672,6 +708,7 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
     o[7] = max_item;
   }
 #endif
+  peer_release(fb.f[0].flags);
   if (lane == 0) {
     uint32_t *done = q.heads + 8 * q.stride;
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
@@ -900,6 +937,7 @@ void render_pump_kernel(P sc, FrameBatch fb, PersistQ q, int32_t nframes, int32_
       live = false;
     }
   }
+  peer_release(F.flags);
   if (lane == 0) {
     uint32_t *done = q.heads + 8 * q.stride;
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q.waves - 1) {
@@ -1055,6 +1093,8 @@ struct rt_scene {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipStream_t xs[2] = {nullptr, nullptr};  // rt_render: colour / t copy streams (render on xs[0])
   hipEvent_t xev = nullptr;
+  int32_t *d_hit_box = nullptr;  // rt_render: FrameArgs::hit_box of its frame (4 words)
+  int32_t *h_hit_box = nullptr;  // pinned host copy of it
   // cost-ordered block schedule (see launch_render): per-block cost of the
   // last frame rendered with sched_grid blocks, and the block order derived
   // from it; sched_on = false renders in plain blockIdx order
@@ -1148,6 +1188,8 @@ int ensure_copy_streams(rt_scene *s) {
   for (hipStream_t &x : s->xs)
     if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   if (!s->xev) HIP_TRY(hipEventCreateWithFlags(&s->xev, hipEventDisableTiming));
+  if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, 4 * sizeof(int32_t)));
+  if (!s->h_hit_box) HIP_TRY(hipHostMalloc(&s->h_hit_box, 4 * sizeof(int32_t), hipHostMallocDefault));
   return RT_OK;
 }
 
@@ -1560,6 +1602,9 @@ int fill_frame(FrameArgs &fa, const rt_render_params *p, uint32_t *c, float *t, 
   fa.rank = 0;
   fa.nranks = 1;
   fa.rows_local = H;
+  fa.order = nullptr;
+  fa.cost = nullptr;
+  fa.hit_box = nullptr;
   if ((flags & RT_FLAG_HITS_ONLY) && !(flags & RT_FLAG_CLEAR))
     return set_err(RT_E_INVALID, "RT_FLAG_HITS_ONLY needs RT_FLAG_CLEAR (a cleared frame)");
   if (flags & ~(RT_FLAG_CLEAR | RT_FLAG_TILE_NATURAL | RT_FLAG_HITS_ONLY))
@@ -1606,10 +1651,15 @@ int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t n
       t_bvh_last = 2;
       return RT_OK;
     }
-    const bool device_failure = err.rfind("GPU BVH build", 0) == 0;
+    if (err.rfind("GPU BVH builder bound", 0) == 0) return set_err(RT_E_DEVICE, err);
+    const bool device_failure = err.rfind("GPU BVH build:", 0) == 0;
     if (!device_failure) return set_err(RT_E_INVALID, err);
     if (g_bvh_mode == RT_BVH_DEVICE) return set_err(RT_E_DEVICE, err);
-    // AUTO: the host builder gives the identical tree
+    // AUTO: the host builder gives the identical tree, unless
+    // the device is left in a sticky fault state: then every later call on it
+    // fails too, so the failure is reported here instead of at the upload
+    if (const hipError_t e = hipDeviceSynchronize(); e != hipSuccess)
+      return set_err(RT_E_DEVICE, err + "; device unusable afterwards: " + hipGetErrorString(e));
     (void)hipGetLastError();
     std::fprintf(stderr, "rtamd: %s; building the BVH on the host instead\n", err.c_str());
     fell_back = true;
@@ -1891,6 +1941,8 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->xev) (void)hipEventDestroy(s->xev);
+  if (s->d_hit_box) (void)hipFree(s->d_hit_box);
+  if (s->h_hit_box) (void)hipHostFree(s->h_hit_box);
   for (hipStream_t x : s->xs)
     if (x) (void)hipStreamDestroy(x);
   (void)hipSetDevice(prev);
@@ -2010,36 +2062,104 @@ int rt_ipc_close(void *d_ptr) {
   return RT_OK;
 }
 
+// rt_render's failure injection (rtx_render_inject_failure): the next n calls
+// fail after their uploads were issued
+std::atomic<int> g_render_fault{0};
+
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
               uint32_t flags, float *ms) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   int rc = check_params(p, W, H);
   if (rc) return rc;
   if (!color || !t) return set_err(RT_E_INVALID, "NULL framebuffer");
+  if (flags & RT_FLAG_TILE_NATURAL) return set_err(RT_E_INVALID, "rt_render renders whole frames (no tile)");
+  // every argument is checked before the first copy is queued
+  FrameArgs fa;
+  if ((rc = fill_frame(fa, p, nullptr, nullptr, W, H, flags & ~RT_FLAG_HITS_ONLY, nullptr))) return rc;
   const size_t px = (size_t)W * H;
   if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s)) || (rc = ensure_copy_streams(s))) return rc;
+  fa.color = s->d_color;
+  fa.t = s->d_t;
   // colour and t move on two streams (two DMA engines; concurrent when the host
-  // buffers are pinned, e.g. by rt_host_pin); a cleared frame (the app's
-  // frameBuf.clear() + draw, RT_FLAG_CLEAR) needs no upload
+  // buffers are pinned, e.g. by rt_host_pin). Once a copy is queued, every
+  // return -- an error included -- first waits for both streams, so the caller
+  // may unpin or free its buffers as soon as the call returns.
   hipStream_t a = s->xs[0], b = s->xs[1];
+  struct Drain {
+    hipStream_t a, b;
+    ~Drain() {
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamSynchronize(b);
+    }
+  } drain{a, b};
+  // Which pixels can differ from the caller's buffers after the frame:
+  //  * RT_FLAG_CLEAR: every pixel (misses become 0 / +inf), so all are copied back;
+  //  * RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY: the caller's buffers already hold a
+  //    cleared frame (the app's frameBuf.clear() + draw, src/main.cpp:197,203),
+  //    so only stored hits differ (raytracing.cpp:91-94);
+  //  * no flag (tPrev frame): colour and t are written only on hit, so again
+  //    only stored hits differ.
+  // In the last two cases the kernel records the bounding box of its stored
+  // pixels and only that box is copied back. The device frame is always
+  // written whole (a cleared frame) or uploaded whole (tPrev), so the box
+  // holds exactly the caller's values outside the hits.
+  const bool boxed = !(flags & RT_FLAG_CLEAR) || (flags & RT_FLAG_HITS_ONLY);
   if (!(flags & RT_FLAG_CLEAR)) {
     HIP_TRY(hipMemcpyAsync(s->d_color, color, px * 4, hipMemcpyHostToDevice, a));
     HIP_TRY(hipMemcpyAsync(s->d_t, t, px * 4, hipMemcpyHostToDevice, b));
     HIP_TRY(hipEventRecord(s->xev, b));
     HIP_TRY(hipStreamWaitEvent(a, s->xev, 0));
   }
-  FrameArgs fa;
-  if ((rc = fill_frame(fa, p, s->d_color, s->d_t, W, H, flags, nullptr))) return rc;
+  if (g_render_fault.load() > 0) {
+    g_render_fault.fetch_sub(1);
+    return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
+  }
+  if (boxed) {
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_hit_box, 0x7FFFFFFF, 4, a));
+    fa.hit_box = s->d_hit_box;
+  }
   HIP_TRY(hipEventRecord(s->ev0, a));
   if ((rc = launch_render(s, fa, a))) return rc;
   HIP_TRY(hipEventRecord(s->ev1, a));
-  HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
-  HIP_TRY(hipMemcpyAsync(t, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
-  HIP_TRY(hipMemcpyAsync(color, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
+  if (!boxed) {
+    HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
+    HIP_TRY(hipMemcpyAsync(t, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
+    HIP_TRY(hipMemcpyAsync(color, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
+  } else {
+    HIP_TRY(hipMemcpyAsync(s->h_hit_box, s->d_hit_box, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, a));
+    HIP_TRY(hipStreamSynchronize(a));
+    const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
+    if (x0 <= x1 && y0 <= y1) {  // else: no hit, nothing changed
+      HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
+      const size_t off = (size_t)y0 * W + x0, rows = (size_t)(y1 - y0 + 1), w = (size_t)(x1 - x0 + 1);
+      if (w * 2 > (size_t)W) {  // wide box: whole rows, one contiguous copy per buffer
+        HIP_TRY(hipMemcpyAsync(t + (size_t)y0 * W, s->d_t + (size_t)y0 * W, rows * W * 4, hipMemcpyDeviceToHost, b));
+        HIP_TRY(hipMemcpyAsync(color + (size_t)y0 * W, s->d_color + (size_t)y0 * W, rows * W * 4,
+                               hipMemcpyDeviceToHost, a));
+      } else {
+        HIP_TRY(hipMemcpy2DAsync(t + off, (size_t)W * 4, s->d_t + off, (size_t)W * 4, w * 4, rows,
+                                 hipMemcpyDeviceToHost, b));
+        HIP_TRY(hipMemcpy2DAsync(color + off, (size_t)W * 4, s->d_color + off, (size_t)W * 4, w * 4, rows,
+                                 hipMemcpyDeviceToHost, a));
+      }
+    }
+  }
   HIP_TRY(hipStreamSynchronize(a));
   HIP_TRY(hipStreamSynchronize(b));
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   return RT_OK;
+}
+
+// test hooks: fail the next n rt_render calls after their uploads; are the
+// scene's copy streams idle?
+int rtx_render_inject_failure(int32_t n) {
+  g_render_fault.store(n);
+  return RT_OK;
+}
+int rtx_render_streams_idle(rt_scene *s) {
+  for (hipStream_t x : s->xs)
+    if (x && hipStreamQuery(x) != hipSuccess) return 0;
+  return 1;
 }
 
 int rt_host_pin(void *ptr, int64_t bytes) {

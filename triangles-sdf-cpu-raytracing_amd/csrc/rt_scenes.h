@@ -154,15 +154,6 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
 #ifndef RT_EXPAND_FAST
 #define RT_EXPAND_FAST 1
 #endif
-// 1: the fast list also covers waves whose rays each enter at most 3 children
-// with distinct t (A/B switch)
-#ifndef RT_SORT3
-#define RT_SORT3 0
-#endif
-// 1: child slots empty in every lane of the wave skip their slab test (A/B switch)
-#ifndef RT_SLOT_SKIP
-#define RT_SLOT_SKIP 0
-#endif
 template <bool FAST>
 __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node, f3 o, f3 inv,
                                             float tNear, float tFar, uint32_t &list,
@@ -181,66 +172,13 @@ __device__ __forceinline__ void expand_node(const rtl::GNode *__restrict__ node,
   uint32_t id[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-#if RT_SLOT_SKIP
-    // an empty slot (child word kInvalidChild, box all +inf: t = -1 for every
-    // ray) in every lane of the wave skips its slab test
-    if (c > 0 && __ballot(cws[c] != rtl::kInvalidChild) == 0) {
-      t[c] = -1.0f;
-      id[c] = (uint32_t)c;
-      continue;
-    }
-#endif
     t[c] = slab<FAST>(bx[6 * c], bx[6 * c + 2], bx[6 * c + 4], bx[6 * c + 1], bx[6 * c + 3],
                       bx[6 * c + 5], o, inv, tNear, tFar);  // box: xMin xMax yMin yMax zMin zMax
     id[c] = (uint32_t)c;
   }
   uint32_t first_id = 0;
   bool sorted = false;
-#if RT_SORT3
-  if constexpr (FAST) {
-    // every lane enters at most 3 children with distinct t: any correct sort
-    // lists them ascending, so a 3-comparator sort of the entered ones gives
-    // the network's list
-    uint32_t m = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) m |= (t[c] < 0.0f) ? 0u : (1u << c);
-    const uint32_t pc = (uint32_t)__builtin_popcount(m);
-    const uint32_t ia = (uint32_t)__builtin_ctz(m | 0x100u), ic = 31u - (uint32_t)__builtin_clz(m | 1u);
-    const uint32_t mb = m & ~(1u << ia) & ~(1u << ic);
-    const uint32_t ib = (uint32_t)__builtin_ctz(mb | 0x100u);
-    float ta = t[0], tb = t[0], tc = t[0];
-#pragma unroll
-    for (int c = 1; c < 8; ++c) {
-      ta = (ia == (uint32_t)c) ? t[c] : ta;
-      tb = (ib == (uint32_t)c) ? t[c] : tb;
-      tc = (ic == (uint32_t)c) ? t[c] : tc;
-    }
-    // entries: pc = 1: a; pc = 2: a, c; pc = 3: a, b, c
-    const bool slow = pc > 3 || (pc >= 2 && !(ta != tc)) || (pc == 3 && (!(ta != tb) || !(tb != tc)));
-    if (__ballot(slow) == 0) {
-      sorted = true;
-      float k0 = ta, k1 = pc == 3 ? tb : tc, k2 = tc;
-      uint32_t d0 = ia, d1 = pc == 3 ? ib : ic, d2 = ic;
-      auto cs = [](float &x, uint32_t &dx, float &y, uint32_t &dy) {
-        const bool sw = x > y;
-        const float tt = x; x = sw ? y : x; y = sw ? tt : y;
-        const uint32_t u = dx; dx = sw ? dy : dx; dy = sw ? u : dy;
-      };
-      if (pc == 3) {
-        cs(k0, d0, k1, d1);
-        cs(k1, d1, k2, d2);
-        cs(k0, d0, k1, d1);
-      } else {
-        cs(k0, d0, k1, d1);  // pc = 2 (k1 = tc); pc <= 1 leaves k0 first
-      }
-      first_id = d0;
-      tfirst = pc == 0 ? 0.0f : k0;
-      cnt = pc;
-      list = pc == 0 ? 0u : pc == 1 ? d0 : pc == 2 ? (d0 | (d1 << 3)) : (d0 | (d1 << 3) | (d2 << 6));
-    }
-  }
-#endif
-  if constexpr (FAST && RT_EXPAND_FAST && !RT_SORT3) {
+  if constexpr (FAST && RT_EXPAND_FAST) {
     // At most two children entered with distinct t: the network's output order
     // of the entered children is plain ascending t (any correct sort gives
     // it), so the wave skips sort8 when every lane is in that case. Ties (or

@@ -57,6 +57,7 @@ class CameraState(C.Structure):
 _SIGS = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (C.c_int, []),
+    "rt_build_id": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),
     "rt_set_device": (C.c_int, [C.c_int]),
     "rt_load_obj": (C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_void_p,
@@ -125,6 +126,21 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
+
+
+def source_build_id() -> str:
+    """rt_build_id() of a library built from this tree (the Makefile's ID_SRCS
+    rule): sha256 of csrc/{*.cpp,*.h,*.hip} in sorted order, then
+    include/rtamd.h; first 16 hex digits."""
+    import glob
+    import hashlib
+    srcs = sorted(os.path.relpath(p, PKG_ROOT) for ext in ("cpp", "h", "hip")
+                  for p in glob.glob(os.path.join(PKG_ROOT, "csrc", f"*.{ext}")))
+    h = hashlib.sha256()
+    for rel in srcs + [os.path.join("..", "include", "rtamd.h")]:
+        with open(os.path.join(PKG_ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def build(force: bool = False) -> str:

@@ -23,7 +23,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (RT_FLAG_CLEAR, CameraState, RenderParams, RtError, Tile, check, lib)
+from ._lib import (RT_FLAG_CLEAR, RT_FLAG_HITS_ONLY, CameraState, RenderParams, RtError, Tile, check, lib)
 
 __all__ = [
     "ShadingMode", "SimpleMesh", "FrameBuffer", "Camera", "Renderer", "HitInfo", "IScene",
@@ -260,14 +260,18 @@ class IScene:
                                       _p(nrm), _p(prim)))
         return HitInfo(hit.astype(bool), t, nrm, prim)
 
-    def render(self, params: RenderParams, color: np.ndarray, t: np.ndarray, clear: bool = False):
-        """Renderer::draw on host buffers; returns the kernel time in ms."""
+    def render(self, params: RenderParams, color: np.ndarray, t: np.ndarray, clear: bool = False,
+               cleared: bool = False):
+        """Renderer::draw on host buffers; returns the kernel time in ms.
+        clear: FrameBuffer::clear() + draw fused (every pixel written);
+        cleared: the buffers already hold a cleared frame (only the hits'
+        bounding box is copied back); neither: t is read as tPrev."""
         H, W = color.shape
         assert color.dtype == np.uint32 and t.dtype == np.float32 and t.shape == color.shape
         assert color.flags.c_contiguous and t.flags.c_contiguous
         ms = C.c_float(0.0)
-        check(lib().rt_render(self._handle(), C.byref(params), _p(color), _p(t), W, H,
-                              RT_FLAG_CLEAR if clear else 0, C.byref(ms)))
+        flags = (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) if cleared else RT_FLAG_CLEAR if clear else 0
+        check(lib().rt_render(self._handle(), C.byref(params), _p(color), _p(t), W, H, flags, C.byref(ms)))
         return ms.value
 
     def render_device(self, params: RenderParams, color_ptr: int, t_ptr: int, W: int, H: int,
