@@ -230,7 +230,9 @@ template <int BLOCK, int F = 3>
 struct LdsStack {
   uint32_t *base;  // lane-interleaved words, F words per frame slot
   __device__ __forceinline__ uint32_t &at(int slot, int field) {
-    return base[(slot * F + field) * BLOCK];
+    // slot * F * BLOCK as a full-rate 24-bit multiply (slots are small): the
+    // plain form compiles to the quarter-rate v_mul_lo_u32
+    return base[__umul24((uint32_t)slot, (uint32_t)(F * BLOCK)) + (uint32_t)(field * BLOCK)];
   }
 };
 
@@ -1012,15 +1014,16 @@ struct OctCorners {
 // (octree_raytracing.cpp:24-25). boxMax - boxMin is exactly the node size s, a
 // power of two (exact dyadic box arithmetic), and x / 2^k == x * 2^-k bit for
 // bit (both round the exact value once, subnormals included), so the three
-// divisions become multiplications by inv_s = 1/s.
+// divisions become multiplications by inv_s = 1/s. p is finite here (a point
+// inside the leaf box), so the clamp is one v_med3 per axis; after it
+// floor(p) = 0 and ceil(p) = 1 on every axis, so p - c0 = p and c1 - p = 1 - p
+// (the reference's subtractions with those operands, the same bits).
 __device__ __forceinline__ void oct_local(f3 bmin, float inv_s, f3 p, f3 &a, f3 &b) {
   p = (p - bmin) * inv_s;
-  p = vstd_min(vstd_max(p, f3{0.0000001f, 0.0000001f, 0.0000001f}),
-               f3{0.9999999f, 0.9999999f, 0.9999999f});
-  const f3 c0{__builtin_floorf(p.x), __builtin_floorf(p.y), __builtin_floorf(p.z)};
-  const f3 c1{__builtin_ceilf(p.x), __builtin_ceilf(p.y), __builtin_ceilf(p.z)};
-  a = p - c0;  // p_c0f  (c0 = 0 and c1 = 1 after the clamp)
-  b = c1 - p;  // c1f_p
+  p = f3{clamp_med3(p.x, 0.0000001f, 0.9999999f), clamp_med3(p.y, 0.0000001f, 0.9999999f),
+         clamp_med3(p.z, 0.0000001f, 0.9999999f)};
+  a = p;                                      // p_c0f = p - 0
+  b = f3{1.0f - p.x, 1.0f - p.y, 1.0f - p.z};  // c1f_p = 1 - p
 }
 
 __device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, float inv_s, f3 p) {
@@ -1060,12 +1063,16 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, float inv
 // point, and oct_normal_at evaluates it after the traversal loop, where the
 // stack state is dead -- the same arithmetic on the same values, outside the
 // loop's register peak.
-template <class CT>
+// FAST (1/d finite, tNear > 0): the box entry with hardware min/max and the
+// start clamp as one v_med3 per axis (t1 is finite, so p is; the clamp's
+// result differs from std's only in the sign of a zero coordinate, which the
+// march's comparisons and oct_local's clamp never see).
+template <bool FAST, class CT>
 __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax,
                                          float inv_s, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                          float &out_t, f3 &out_p, CT &cnt) {
   float t1, t2;
-  bbox_intersection(bmin, bmax, o, inv, tNear, tFar, t1, t2);
+  bbox_isect<FAST>(bmin, bmax, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
   OctCorners c;
   const float4 *q = reinterpret_cast<const float4 *>(sc.vals + node);
@@ -1074,10 +1081,20 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   c.v[4] = b.x; c.v[5] = b.y; c.v[6] = b.z; c.v[7] = b.w;
   float t = t1;
   f3 p = o + t * d;
-  p = vstd_max(p, bmin);
-  p = vstd_min(p, bmax);
-  while (p.x <= bmax.x && p.y <= bmax.y && p.z <= bmax.z && p.x >= bmin.x && p.y >= bmin.y &&
-         p.z >= bmin.z) {
+  if constexpr (FAST) {
+    p = f3{clamp_med3(p.x, bmin.x, bmax.x), clamp_med3(p.y, bmin.y, bmax.y), clamp_med3(p.z, bmin.z, bmax.z)};
+  } else {
+    p = vstd_max(p, bmin);
+    p = vstd_min(p, bmax);
+  }
+  // p inside the box on every axis, as med3(p, min, max) == p: false for a NaN
+  // coordinate, true exactly when min <= p <= max (3 med3 + 3 compares instead
+  // of 6 compares and their mask ands)
+  auto inside = [&](f3 q) {
+    return clamp_med3(q.x, bmin.x, bmax.x) == q.x && clamp_med3(q.y, bmin.y, bmax.y) == q.y &&
+           clamp_med3(q.z, bmin.z, bmax.z) == q.z;
+  };
+  while (inside(p)) {
     const float s = oct_sdf(c, bmin, inv_s, p);
     cnt.add(C_OCT_STEP, 1);
     if (s < 1e-4f) {
@@ -1311,8 +1328,8 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
     cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return RAY_MISS;
     hp.node = 0; hp.ix = 0; hp.iy = 0; hp.iz = 0; hp.depth = 0;
-    return oct_leaf(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar, out_t,
-                    hp.p, cnt)
+    return oct_leaf<FAST>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar,
+                          out_t, hp.p, cnt)
                ? RAY_HIT
                : RAY_MISS;
   }
@@ -1375,7 +1392,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     oct_box(cxyz.ix(), cxyz.iy(), cxyz.iz(), depth + 1, bmin, bmax, inv_s);
     if (leaf) {
       cnt.add(C_OCT_LEAF, 1);
-      if (oct_leaf(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, hp.p, cnt)) {
+      if (oct_leaf<FAST>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, hp.p, cnt)) {
         hp.node = cn; hp.ix = cxyz.ix(); hp.iy = cxyz.iy(); hp.iz = cxyz.iz(); hp.depth = depth + 1;
         return RAY_HIT;
       }
