@@ -77,3 +77,47 @@ def test_grid_layout_rays(gpu, size):
     h = g.hitten
     assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
     assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
+
+
+def _batch_frames(gs, params, W, H):
+    """Frames through rt_render_device_frames (the multi-frame block dispatch the
+    bench times), read back to the host."""
+    import torch
+    n = len(params)
+    cs = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(n)]
+    ts = [torch.empty((H, W), dtype=torch.float32, device="cuda") for _ in range(n)]
+    gs.render_device_frames(params, [c.data_ptr() for c in cs], [t.data_ptr() for t in ts], W, H, rtamd.RT_FLAG_CLEAR)
+    torch.cuda.synchronize()
+    return [(c.cpu().numpy().view(np.uint32), t.cpu().numpy()) for c, t in zip(cs, ts)]
+
+
+@pytest.mark.parametrize("size", [(103, 97, 130), (24, 24, 24), (65, 65, 65)])
+@pytest.mark.parametrize("mode", ["primary", "default"])
+def test_grid_lds_block_cache_frames(gpu, size, mode):
+    """The per-wave LDS block cache of the march (kGridLds, rtx_set_grid_lds):
+    multi-frame launches on the bricked (103x97x130) and linear (24^3, 65^3)
+    layouts equal the oracle's frames bit for bit, with the cache on and off,
+    including the default mode's shadow and reflection rays (which march
+    through the same cache)."""
+    import ctypes as C
+    sz, vals = sdf_grid(size, zlib.crc32(repr(size).encode()) + 1)
+    ref_s, gpu_s = cpuref.RefScene.grid(sz, vals), rtamd.SDFGrid(sz, vals)
+    L = rtamd.lib()
+    L.rtx_set_grid_lds.argtypes = [C.c_void_p, C.c_int]
+    sm, plane = {"primary": (0, False), "default": (1, True)}[mode]
+    ref_s.set_plane(plane, (0.0, 1.0, 0.0), -0.8)
+    gpu_s.set_plane(rtamd.Plane((0.0, 1.0, 0.0), -0.8) if plane else None)
+    W, H = 160, 120
+    poses = [(0.0, 0.5, 2.5), (2.0, -0.7, -1.2), (0.3, 0.2, 0.4), (-1.1, 1.4, 1.7), (0.9, 0.0, -2.2)]
+    gp, rp = [], []
+    for pos in poses:
+        vi, pi = cpuref.camera_matrices(pos, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 45.0, W / H, 0.01, 100.0)
+        gp.append(rtamd.render_params(pos, vi, pi, (2, 2, 2), sm, True, True))
+        rp.append(cpuref.make_params(pos, vi, pi, (2, 2, 2), sm, True, True))
+    refs = [ref_s.render(p, W, H)[:2] for p in rp]
+    gpu_s.render(gp[0], np.zeros((H, W), np.uint32), np.full((H, W), np.inf, np.float32), clear=True)  # create
+    for on in (1, 0):
+        rtamd._lib.check(L.rtx_set_grid_lds(gpu_s._h, on))
+        for k, ((gc, gt), (rc, rt_)) in enumerate(zip(_batch_frames(gpu_s, gp, W, H), refs)):
+            assert np.array_equal(rc, gc), f"lds={on} {size} {mode} frame {k}: {(rc != gc).sum()} px differ"
+            assert np.array_equal(rt_.view(np.uint32), gt.view(np.uint32)), f"lds={on} {size} {mode} frame {k}: t"

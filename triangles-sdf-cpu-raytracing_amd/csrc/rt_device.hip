@@ -97,6 +97,7 @@ struct FrameArgs {
 #endif
 struct MeshS {
   static constexpr int kFields = 3;
+  static constexpr bool kWaveInit = false;
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   static constexpr int kMinWaves = RT_MESH_WAVES;
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
@@ -129,7 +130,11 @@ struct MeshS {
 };
 template <int kMode>
 struct GridS {
-  static constexpr int kFields = 1;
+  // no traversal stack (one unused LDS word per lane); with kGridLds the wave's
+  // LDS block cache: kFields words per lane, used as one contiguous region per
+  // wave (grid_lds_region)
+  static constexpr int kFields = (kMode & kGridLds) ? (kGridLdsWords + 63) / 64 : 1;
+  static constexpr bool kWaveInit = (kMode & kGridLds) != 0;  // the block cache's tags start empty
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_GRID_WAVES;
   // block dispatch: a grid tile is too short for the queue's claims to pay
@@ -137,15 +142,29 @@ struct GridS {
   static constexpr int kQueueGroup = 0;
   static constexpr int kLdsNodes = 0;
   GridDev d;
+  // the wave's contiguous kFields * 64 words of the block's stack array (the
+  // stack is lane-interleaved from stk + threadIdx.x; the grid has no stack)
+  template <int B>
+  __device__ __forceinline__ static float *grid_lds_region(LdsStack<B, kFields> st) {
+    uint32_t *blk = st.base - threadIdx.x;
+    return reinterpret_cast<float *>(blk + (threadIdx.x >> 6) * (kFields * 64));
+  }
+  // every lane of the wave, before its tile: the cache's 8 tags empty (LDS
+  // keeps the previous workgroup's words)
+  template <int B>
+  __device__ __forceinline__ static void wave_init(uint32_t *stk) {
+    uint32_t *region = stk + (threadIdx.x >> 6) * (kFields * 64);
+    if ((threadIdx.x & 63) < kGridLdsSlots) region[kGridLdsSlots * kGridLdsBlk + (threadIdx.x & 63)] = 0u;
+  }
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
-                                           LdsStack<B, kFields>, CT &cnt) const {
-    return grid_intersect<kMode>(d, o, dir, tn, tf, cnt);
+                                           LdsStack<B, kFields> st, CT &cnt) const {
+    return grid_intersect<kMode>(d, o, dir, tn, tf, cnt, (kMode & kGridLds) ? grid_lds_region<B>(st) : nullptr);
   }
   template <int B, class CT>
   __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
-                                           LdsStack<B, kFields>, CT &cnt) const {
-    return grid_occluded<kMode>(d, o, dir, tn, tf, cnt);
+                                           LdsStack<B, kFields> st, CT &cnt) const {
+    return grid_occluded<kMode>(d, o, dir, tn, tf, cnt, (kMode & kGridLds) ? grid_lds_region<B>(st) : nullptr);
   }
 };
 // PACK: the traversal carries the node coordinates packed in one register
@@ -153,6 +172,7 @@ struct GridS {
 template <bool PACK>
 struct OctS {
   static constexpr int kFields = kOctFields;
+  static constexpr bool kWaveInit = false;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   static constexpr int kQueueGroup = 2;
@@ -356,6 +376,7 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
   const bool active = xo < fa.W && yl < fa.rows_local;
   // wave-cooperative primary path: every lane of the wave takes part
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
+  if constexpr (S::kWaveInit) S::template wave_init<B>(stk);  // (all lanes of the wave are here)
   if (DIAG == 0 && !kWaveCoop && !active) return false;
   if (active || kWaveCoop) {  // (the counting variant keeps every lane for its wave reduction)
     LdsStack<B, S::kFields> st{stk + threadIdx.x};
@@ -1104,6 +1125,12 @@ struct rt_scene {
   uint32_t sched_grid = 0;
   bool sched_on = true;
   bool coop = true;  // mesh primary rays: cooperative tail (rtx_set_coop)
+  // grid: multi-frame launches march through the per-wave LDS block cache
+  // (kGridLds; rtx_set_grid_lds, RTAMD_GRID_LDS=1 for new scenes)
+  bool grid_lds = [] {
+    const char *e = std::getenv("RTAMD_GRID_LDS");
+    return e && e[0] == '1';
+  }();
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
@@ -1496,7 +1523,7 @@ struct PumpOf<OctS<PK>> {
 };
 template <int kMode>
 struct PumpOf<GridS<kMode>> {
-  static constexpr bool kHas = true;
+  static constexpr bool kHas = (kMode & kGridLds) == 0;  // (the block cache is the tile kernels')
   using P = GridP<kMode>;
   static P make(const GridS<kMode> &s) { return P{s.d}; }
 };
@@ -1560,7 +1587,15 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
     }
   } else if (s->kind == RT_SCENE_GRID) {
     const GridDev gd = grid_dev(s);
-    switch (grid_mode(s, gd)) {
+    const int mode = grid_mode(s, gd);
+    // the LDS block cache (rtx_set_grid_lds / RTAMD_GRID_LDS; A/B switch, buffer modes only)
+    switch ((s->grid_lds && (mode & kGridBuf)) ? (mode | kGridLds) : mode) {
+      case kGridBuf | kGridBricked | kGridLds:
+        rc = launch_batch_t<GridS<kGridBuf | kGridBricked | kGridLds>, 1>(s, {gd}, s->plane, fb, n, general, stream);
+        break;
+      case kGridBuf | kGridLds:
+        rc = launch_batch_t<GridS<kGridBuf | kGridLds>, 1>(s, {gd}, s->plane, fb, n, general, stream);
+        break;
       case kGridBuf | kGridBricked:
         rc = launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>(s, {gd}, s->plane, fb, n, general, stream);
         break;
@@ -2433,6 +2468,12 @@ int rtx_set_coop(rt_scene *s, int on) {
 
 // Diagnostic switch: primary-ray batches of this scene on the ray pump
 // (render_pump_kernel) instead of one tile per wave (default off).
+int rtx_set_grid_lds(rt_scene *s, int on) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  s->grid_lds = on != 0;
+  return RT_OK;
+}
+
 int rtx_set_pump(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   s->pump_on = on != 0;
