@@ -37,15 +37,22 @@ utilisation. `one_stream` repeats the launches on ONE stream, where a launch's
 HIP-event duration is its own (rocprofv3's average for the kernel must agree).
 Raw counters go to the --detail file, not the JSON line.
 
-Multi-GPU (torch.distributed.run, one process per GPU; rtamd.rowsplit): every
-frame is split into --band-rows (8) row bands dealt round-robin to the ranks.
-Exchange p2p (default): each rank's kernel stores its HIT pixels straight into
-rank 0's frame slots over xGMI (IPC-mapped) and one 4-byte RCCL all-reduce per
-group signals completion; exchange gather: one RCCL gather per group of packed
-bands + a de-interleave on rank 0. The frame is fixed as N grows ("strong");
-value = pixels of all frames / max-over-ranks wall time. Every rank reports
-its render-kernel time (rank_kernel_ms). rank 0 checks that its last assembled
-frame equals a whole-frame render.
+Multi-GPU (one process per GPU; rtamd.rowsplit): `--gpus N` under
+torch.distributed.run, or run directly: without WORLD_SIZE in the environment
+this process spawns the N rank processes itself (spawn_ranks, before anything
+touches the GPU), relays rank 0's line and exits with the worst rank's code; a
+GPU count it cannot run is an error, never a 1-GPU line. Every frame is split
+into --band-rows (8) row bands dealt round-robin to the ranks. Exchange p2p
+(default): each rank's kernel stores its HIT pixels straight into rank 0's
+frame slots over xGMI (IPC-mapped), each wave ending with a system-scope
+release, and one 4-byte RCCL all-reduce per group signals completion; exchange
+gather: one RCCL gather per group of packed bands + a de-interleave on rank 0.
+The frame is fixed as N grows ("strong"); value = pixels of all frames /
+max-over-ranks wall time. Every rank reports its render-kernel time
+(rank_kernel_ms). The warm-up is a verification pass: every slot group is
+reused at least twice and EVERY assembled frame of it is compared bitwise
+with a whole-frame render on rank 0 (frame_check.verify_pass), and so is the
+last timed frame.
 
 drop_in (N=1): rt_render, the Renderer::draw surface INTEGRATION.md binds, on
 HOST buffers (upload when not cleared, render, download), ms per frame with the
