@@ -259,13 +259,13 @@ def test_drop_in_partial_download(gpu, pinned):
 
 def test_drop_in_failure_leaves_no_copy_in_flight(gpu):
     """An rt_render that fails after queueing its uploads (injected) returns
-    only once its copy streams are idle, so pinned buffers can be unpinned and
-    freed at once; the next call renders normally."""
+    only after synchronising both copy streams, so pinned buffers can be
+    unpinned and freed at once; the next call renders normally."""
     import ctypes as C
     rt = gpu
     L = rt.lib()
     L.rtx_render_inject_failure.argtypes = [C.c_int32]
-    L.rtx_render_streams_idle.argtypes = [C.c_void_p]
+    L.rtx_render_drain_count.restype = C.c_int64
     name, W, H = "stanford-bunny.obj", 1920, 1080
     sc = S.gpu_scene(name)
     S.set_planes(name, "primary", sc)
@@ -276,9 +276,11 @@ def test_drop_in_failure_leaves_no_copy_in_flight(gpu):
     P = S.params(name, W, H, "primary", (0.0, 0.0, 2.5), "gpu")
     try:
         L.rtx_render_inject_failure(1)
+        n0 = L.rtx_render_drain_count()
         with pytest.raises(rt.RtError, match="injected"):
             sc.render(P, c, t, clear=False)  # tPrev: both uploads queued before the failure
-        assert L.rtx_render_streams_idle(sc._h) == 1
+        # the failing return synchronised both copy streams (successfully)
+        assert L.rtx_render_drain_count() == n0 + 1
     finally:
         L.rtx_render_inject_failure(0)
         L.rt_host_unpin(c.ctypes.data)

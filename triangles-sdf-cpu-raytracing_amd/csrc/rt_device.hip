@@ -2098,8 +2098,10 @@ int rt_ipc_close(void *d_ptr) {
 }
 
 // rt_render's failure injection (rtx_render_inject_failure): the next n calls
-// fail after their uploads were issued
+// fail after their uploads were issued; g_render_drains counts the returns that
+// waited for both copy streams (rtx_render_drain_count)
 std::atomic<int> g_render_fault{0};
+std::atomic<int64_t> g_render_drains{0};
 
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
               uint32_t flags, float *ms) {
@@ -2123,8 +2125,8 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   struct Drain {
     hipStream_t a, b;
     ~Drain() {
-      (void)hipStreamSynchronize(a);
-      (void)hipStreamSynchronize(b);
+      const hipError_t ea = hipStreamSynchronize(a), eb = hipStreamSynchronize(b);
+      if (ea == hipSuccess && eb == hipSuccess) g_render_drains.fetch_add(1);
     }
   } drain{a, b};
   // Which pixels can differ from the caller's buffers after the frame:
@@ -2185,17 +2187,13 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   return RT_OK;
 }
 
-// test hooks: fail the next n rt_render calls after their uploads; are the
-// scene's copy streams idle?
+// test hooks: fail the next n rt_render calls after their uploads; how many
+// rt_render returns have waited for both copy streams
 int rtx_render_inject_failure(int32_t n) {
   g_render_fault.store(n);
   return RT_OK;
 }
-int rtx_render_streams_idle(rt_scene *s) {
-  for (hipStream_t x : s->xs)
-    if (x && hipStreamQuery(x) != hipSuccess) return 0;
-  return 1;
-}
+int64_t rtx_render_drain_count(void) { return g_render_drains.load(); }
 
 int rt_host_pin(void *ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad host range");
