@@ -173,3 +173,21 @@ def test_auto_mode_falls_back_to_host_on_device_failure(gpu):
     finally:
         L.rtx_bvh_inject_failure(0)
         rtamd._lib.check(L.rt_set_bvh_builder(0))
+
+
+def test_auto_mode_reports_builder_bounds(gpu):
+    """An exceeded bound of the device builder's own stage logic (a builder bug,
+    simulated by rtx_bvh_inject_failure(-1)) is reported as RT_E_DEVICE in AUTO
+    mode too, not hidden by the host fallback; the next build is unaffected."""
+    import rtamd
+    L = rtamd.lib()
+    _, (v, i), _ = S.inputs("stanford-bunny.obj")
+    L.rtx_bvh_inject_failure(-1)
+    try:
+        with pytest.raises(rtamd.RtError, match=r"error -3: GPU BVH builder bound: injected bound"):
+            rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    finally:
+        L.rtx_bvh_inject_failure(0)
+    sc = rtamd.BVHBuilder(rtamd.SimpleMesh(v, i))
+    assert L.rtx_bvh_last_builder() == 2
+    sc.close()

@@ -1095,9 +1095,13 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   if ((uint64_t)n > rtl::kMaxLeafFirstTri || 3ull * n >= (1ull << 31)) { err = "too many triangles"; return false; }
   out = BVHGpu();
   if (n == 0) { out.root_word = rtl::kInvalidChild; return true; }
-  if (g_inject_fail.load() > 0) {  // rtx_bvh_inject_failure: a simulated device failure
-    g_inject_fail.fetch_sub(1);
-    return hfail("injected failure", hipErrorOutOfMemory);
+  if (const int inj = g_inject_fail.load(); inj != 0) {  // rtx_bvh_inject_failure
+    g_inject_fail.fetch_add(inj > 0 ? -1 : 1);
+    if (inj < 0) {  // a simulated builder bug: never hidden by the host fallback
+      err = "GPU BVH builder bound: injected bound";
+      return false;
+    }
+    return hfail("injected failure", hipErrorOutOfMemory);  // a simulated device failure
   }
 
   const auto tb0 = std::chrono::steady_clock::now();
@@ -1315,10 +1319,11 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
 // ---- diagnostics (not part of include/rtamd.h) ------------------------------
 extern "C" {
 
-// Fault injection for the builder fallback test: the next `n` device builds
-// fail with a device error before touching the GPU.
+// Fault injection for the builder fallback tests: the next |n| device builds
+// fail before touching the GPU, with a device error (n > 0) or with an
+// exceeded bound of the builder's own stage logic (n < 0).
 int rtx_bvh_inject_failure(int32_t n) {
-  g_inject_fail.store(n < 0 ? 0 : n);
+  g_inject_fail.store(n);
   return RT_OK;
 }
 

@@ -41,6 +41,10 @@ namespace {
 inline int set_err(int code, const std::string &msg) { return rterr::set(code, msg); }
 
 constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
+// Coop threshold of a persistent wave's last item (0: the same as every item's)
+#ifndef RT_TAIL_COOP
+#define RT_TAIL_COOP 0
+#endif
 // Workgroup of the persistent multi-frame kernel (render_persist_kernel), in
 // threads. Its waves are independent (each pulls its own items), so the block
 // only sets the granularity at which a launch's resources are handed back:
@@ -103,13 +107,16 @@ struct MeshS {
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
   static constexpr int kLdsNodes = RT_LDS_NODES;  // top-of-tree nodes per persistent block in LDS
   MeshDev d;
+  // rays at or below which the wave hands its remaining rays to 8-lane groups
+  // (wave-uniform; the persistent kernel raises it for a wave's last item)
+  int coop_rays = kCoopRays;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
                                          uint32_t *stk) const {
     float t;
     uint32_t k;
     Hit h = miss_hit();
-    if (mesh_primary_wave<B>(d, o, dir, tn, tf, active, stk, t, k) && active) {
+    if (mesh_primary_wave<B>(d, o, dir, tn, tf, active, stk, t, k, coop_rays) && active) {
       h.hit = true;
       h.t = t;
       h.n = tri_normal(d.tris, k);
@@ -688,6 +695,13 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
       k = knext;
       continue;
     }
+#if RT_TAIL_COOP
+    // the launch's tail: this wave's head has no item after this one, so the
+    // wave runs with few others and its heavy rays are issue-bound; hand its
+    // last RT_TAIL_COOP rays to 8-lane groups (rounds of 8) instead of 8
+    if constexpr (S::kCoop && !GENERAL)
+      sc.coop_rays = (q.cpf == 0 ? knext * 8 + h >= q.items : knext >= q.nper) ? RT_TAIL_COOP : kCoopRays;
+#endif
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
 #ifdef RT_PERSIST_STAMPS
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();

@@ -300,14 +300,14 @@ constexpr int kCoopRays = RT_COOP_RAYS;
 // of the wave are still looping, store the state and return true (suspended).
 template <int BLOCK, bool ANY, bool FAST, bool TAIL, uint32_t LB = RT_LEAF_BATCH, class CT>
 __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                         LdsStack<BLOCK> st, MState &S, CT &cnt) {
+                                         LdsStack<BLOCK> st, MState &S, CT &cnt, int coop_rays = kCoopRays) {
   uint32_t word = S.word, flist = S.flist, fcnt = S.fcnt, fnode = S.fnode, cwnext = S.cwnext, gk = S.gk;
   float fbest = S.fbest, tnext = S.tnext, gbest = S.gbest;
   int depth = S.depth;
   bool have_t = S.have_t;
   bool suspended = false;
   for (;;) {
-    if (TAIL && __popcll(__ballot(1)) <= kCoopRays) { suspended = true; break; }
+    if (TAIL && __popcll(__ballot(1)) <= coop_rays) { suspended = true; break; }
     if (word != rtl::kInvalidChild) {
       if (word & rtl::kLeafBit) {
         float lt = kInf;
@@ -586,7 +586,7 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
 template <int BLOCK>
 __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
                                                   bool active, uint32_t *stk_block, float &out_t,
-                                                  uint32_t &out_k) {
+                                                  uint32_t &out_k, int coop_rays = kCoopRays) {
   NoCnt cnt;
   const int lane = threadIdx.x & 63;
   LdsStack<BLOCK> st{stk_block + threadIdx.x};
@@ -612,8 +612,10 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   }
   bool suspended = false;
   if (pending && sc.coop)
-    suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
-                     : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt);
+    suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
+                                                                                  coop_rays)
+                     : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
+                                                                                   coop_rays);
   else if (pending)
     (void)(fast ? mesh_run<BLOCK, false, true, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
                 : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt));
