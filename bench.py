@@ -801,6 +801,8 @@ def main():
                    if use_dist else "1 GPU, 1 thread per pixel",
                    "frames_per_launch": a.group, "streams": a.streams},
         "roofline": rl,
+        # sha256 of the loaded library's sources (rt_build_id): ties the line to a source tree
+        "build_id": rtamd.lib().rt_build_id().decode(),
     }
     if frame_ok is not None:
         out["frame_check"] = {"last_timed_frame_equals_one_frame_kernel": frame_ok}
