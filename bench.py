@@ -8,7 +8,8 @@ stanford-bunny.obj at 1920x1080, primary rays = Normal shading, no ground plane,
 one ray per pixel, the pure intersection hot path); every key of WORKLOADS
 works at every N, e.g. `--workload mesh_large` is configs[4] (the 1.1 M-triangle
 stand-in at 3840x2160) and `--workload grid` configs[2] (the 256^3 stand-in).
-Orbit frames are independent: up to --group (8) of them go out in ONE launch
+Orbit frames are independent: up to --group of them (8 on one GPU, 16 per
+rank at N > 1, where a rank's share of a frame is 1/N) go out in ONE launch
 (the persistent kernel pulls 8x8 pixel tiles of all of them from one work
 queue) and launches alternate over --streams (2) HIP streams with their own
 framebuffers. value = rays of all K frames / wall time of the K frames.
@@ -130,8 +131,9 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
                     help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
-    ap.add_argument("--group", type=int, default=8,
-                    help="frames per launch (at most 8); N>1: also per completion signal / gather")
+    ap.add_argument("--group", type=int, default=None,
+                    help="frames per launch (at most 16; default 8 on one GPU, 16 per rank at N>1); "
+                         "N>1: also per completion signal / gather")
     ap.add_argument("--depth", type=int, default=3, help="N>1: groups whose slots are in flight")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the launches alternate over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -698,8 +700,10 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     a = parse()
-    if not 1 <= a.group <= 8:
-        raise SystemExit("--group must be 1..8 (frames per launch)")
+    if a.group is None:  # 8 whole frames per launch; a row-band rank renders 1/N of each, so 16
+        a.group = 16 if int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.gpus > 1 else 8
+    if not 1 <= a.group <= 16:
+        raise SystemExit("--group must be 1..16 (frames per launch)")
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     key, entry = workload_entry(a.workload)

@@ -185,7 +185,7 @@ int rt_untile_device(const uint32_t *d_packed_color, const float *d_packed_t, in
 /* Pixels a rank owns under `tile` (its packed buffer length). */
 int64_t rt_tile_pixels(int32_t W, int32_t H, const rt_tile *tile);
 /* rt_render_device for `frames` frames of one size/tile/shading path, on
- * `stream`: frame f uses params[f], d_color[f], d_t[f]. Up to 8 frames share
+ * `stream`: frame f uses params[f], d_color[f], d_t[f]. Up to 16 frames share
  * ONE launch (blockIdx.z = frame), so each frame's silhouette tail is covered
  * by the next frames' tiles; the image of every frame is identical to
  * rt_render_device's. */

@@ -275,6 +275,54 @@ def test_schedule_state_is_output_neutral(gpu):
             assert_same(S.ref_frame(name, W, H, "primary", pos), outs[(1, k)], f"schedule frame {k}")
 
 
+def test_sixteen_frames_per_launch(gpu):
+    """16 frames in ONE rt_render_device_frames launch (the multi-GPU ranks'
+    launch size): whole frames through the persistent kernel and one rank's
+    packed row bands through the block dispatch equal the frames rendered
+    one at a time, bit for bit (and the first whole frames equal the oracle)."""
+    import ctypes as C
+
+    import rtamd
+    from rtamd._lib import lib
+    torch = pytest.importorskip("torch")
+    from rtamd.workloads import orbit_positions
+    L = lib()
+    name = "stanford-bunny.obj"
+    s = S.gpu_scene(name)
+    S.set_planes(name, "primary", s)
+    W, H, n = 320, 180, 16
+    pos = orbit_positions(64)[:n]
+    P = [S.params(name, W, H, "primary", p, module="gpu") for p in pos]
+    single = []
+    for prm in P:
+        c = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+        s.render_device(prm, c.data_ptr(), t.data_ptr(), W, H, clear=True)
+        torch.cuda.synchronize()
+        single.append((c.cpu().numpy().view(np.uint32), t.cpu().numpy().view(np.uint32)))
+    cs = [torch.zeros((H, W), dtype=torch.int32, device="cuda") for _ in P]
+    ts = [torch.zeros((H, W), dtype=torch.float32, device="cuda") for _ in P]
+    s.render_device_frames(P, [c.data_ptr() for c in cs], [t.data_ptr() for t in ts], W, H, rtamd.RT_FLAG_CLEAR)
+    torch.cuda.synchronize()
+    for k in range(n):
+        assert np.array_equal(cs[k].cpu().numpy().view(np.uint32), single[k][0]), k
+        assert np.array_equal(ts[k].cpu().numpy().view(np.uint32), single[k][1]), k
+    for k in range(2):
+        assert_same(S.ref_frame(name, W, H, "primary", pos[k]), (cs[k].cpu().numpy().view(np.uint32),
+                                                                  ts[k].cpu().numpy()), f"16-frame launch {k}")
+    tile = rtamd.Tile(8, 1, 3, 0)
+    npx = L.rt_tile_pixels(W, H, C.byref(tile))
+    pc = [torch.zeros(npx, dtype=torch.int32, device="cuda") for _ in P]
+    pt = [torch.zeros(npx, dtype=torch.float32, device="cuda") for _ in P]
+    s.render_device_frames(P, [c.data_ptr() for c in pc], [t.data_ptr() for t in pt], W, H, rtamd.RT_FLAG_CLEAR,
+                           tile=tile)
+    torch.cuda.synchronize()
+    rows = [y for y in range(H) if (y // 8) % 3 == 1]
+    for k in range(n):
+        assert np.array_equal(pc[k].cpu().numpy().view(np.uint32), single[k][0][rows].reshape(-1)), k
+        assert np.array_equal(pt[k].cpu().numpy().view(np.uint32), single[k][1][rows].reshape(-1)), k
+
+
 SORT8_PAIRS = [(0, 1), (2, 3), (4, 5), (6, 7), (0, 2), (1, 3), (4, 6), (5, 7), (1, 2), (5, 6),
                (0, 4), (3, 7), (1, 5), (2, 6), (1, 4), (3, 6), (2, 4), (3, 5), (3, 4)]
 

@@ -7,7 +7,8 @@ launch machinery, so numbers are comparable with the bench).
                                             renderer: EVERY rank r of N renders
                                             its 8-row bands (AB_NS="2,4,8"); the
                                             max over ranks bounds the N-GPU scaling;
-                                            AB_STREAMS: streams per rank, default 2
+                                            AB_STREAMS: streams per rank, default 2;
+                                            AB_GROUP: frames per launch, default 8
   python tools/ab.py modes [workload ...]   primary and default shading
 
 workload: a key of bench.WORKLOADS (bunny, grid, grid_shipped, octree,
@@ -63,16 +64,17 @@ def main():
         elif what == "split":
             sc.set_plane(None)
             prm = bench.orbit_params(WARM + STEPS, W, H)
-            base, _ = timed(sc, prm, W, H, 2, 8)
+            group = int(os.environ.get("AB_GROUP", "8"))  # frames per launch (<= the build's RT_MAX_BATCH)
+            base, _ = timed(sc, prm, W, H, 2, group)
             print(f"{name} N=1: {base:.4f} ms/frame", flush=True)
             for n in (int(x) for x in os.environ.get("AB_NS", "2,4,8").split(",")):
                 per = []
                 for r in range(n):
-                    ms, kms = timed(sc, prm, W, H, int(os.environ.get("AB_STREAMS", "2")), 8,
+                    ms, kms = timed(sc, prm, W, H, int(os.environ.get("AB_STREAMS", "2")), group,
                                     _lib.Tile(8, r, n, 0))
                     per.append((ms, kms))
                     print(f"{name} N={n} rank {r}: {ms:.4f} ms/frame ({base / ms:.2f}x of N=1), "
-                          f"{kms:.4f} ms/launch of 8", flush=True)
+                          f"{kms:.4f} ms/launch of {group}", flush=True)
                 worst = max(ms for ms, _ in per)
                 print(f"{name} N={n}: max over ranks {worst:.4f} ms/frame -> compute-side bound "
                       f"{base / worst:.2f}x", flush=True)

@@ -553,8 +553,12 @@ void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
 // silhouette, the per-frame tail) finish, so only the batch's last frame
 // leaves a tail. The per-frame arguments travel in the kernarg segment
 // (uniform blockIdx.z index: scalar loads).
+// At most 16 frames per launch (3.7 KiB of kernel arguments): row-band ranks
+// of a multi-GPU split render 1/N of each frame, so they take 16 frames per
+// launch to keep a launch's bulk long against its tail (bench.py --group;
+// rank compute at N = 8: 0.0170 -> 0.0133 ms/frame); whole frames stay at 8.
 #ifndef RT_MAX_BATCH
-#define RT_MAX_BATCH 8
+#define RT_MAX_BATCH 16
 #endif
 constexpr int kMaxBatch = RT_MAX_BATCH;
 struct FrameBatch {

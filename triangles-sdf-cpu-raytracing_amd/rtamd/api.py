@@ -286,7 +286,7 @@ class IScene:
 
     def render_device_frames(self, params_list, color_ptrs, t_ptrs, W: int, H: int, flags: int,
                              tile: Tile | None = None, stream: int | None = None):
-        """rt_render_device_frames: up to 8 frames per launch, one host call."""
+        """rt_render_device_frames: up to 16 frames per launch, one host call."""
         n = len(params_list)
         arr = (RenderParams * n)(*params_list)
         cp = (C.c_void_p * n)(*color_ptrs)
