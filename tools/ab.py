@@ -31,7 +31,7 @@ import rtamd  # noqa: E402
 from rtamd import _lib  # noqa: E402
 from rtamd import workloads as WL  # noqa: E402
 
-WARM, STEPS = 16, 128
+WARM, STEPS = int(os.environ.get("AB_WARM", "16")), int(os.environ.get("AB_STEPS", "128"))
 
 
 def resolve(name):
