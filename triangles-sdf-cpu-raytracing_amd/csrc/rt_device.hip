@@ -110,13 +110,16 @@ struct MeshS {
   // rays at or below which the wave hands its remaining rays to 8-lane groups
   // (wave-uniform; the persistent kernel raises it for a wave's last item)
   int coop_rays = kCoopRays;
+  // traversal iterations after which a wave raises its priority (0: never;
+  // the persistent kernel sets RT_HEAVY_PRIO, the one-frame kernel keeps 0)
+  int prio_iters = 0;
   template <int B>
   __device__ __forceinline__ Hit primary(f3 o, f3 dir, float tn, float tf, bool active,
                                          uint32_t *stk) const {
     float t;
     uint32_t k;
     Hit h = miss_hit();
-    if (mesh_primary_wave<B>(d, o, dir, tn, tf, active, stk, t, k, coop_rays) && active) {
+    if (mesh_primary_wave<B>(d, o, dir, tn, tf, active, stk, t, k, coop_rays, prio_iters) && active) {
       h.hit = true;
       h.t = t;
       h.n = tri_normal(d.tris, k);
@@ -641,6 +644,7 @@ __global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(min_wav
 void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
   __shared__ uint32_t stk[SLOTS * S::kFields * kPBlock];
   S sc = sc_arg;
+  if constexpr (S::kCoop && !GENERAL) sc.prio_iters = RT_HEAVY_PRIO;
   if constexpr (S::kLdsNodes > 0 && !GENERAL) {
     // the top BVH levels (the first inner nodes, BFS order) copied into this
     // block's LDS once per launch; every item's traversal reads them there

@@ -292,6 +292,15 @@ struct MState {
 #define RT_COOP_RAYS 8  // A/B switch (0: never hand over)
 #endif
 constexpr int kCoopRays = RT_COOP_RAYS;
+// Persistent primary-mesh waves still traversing a tile after this many
+// iterations (a silhouette tile: the chains that end a launch) raise their
+// issue priority on their SIMD until the tile is done (0: off; A/B switch)
+#ifndef RT_HEAVY_PRIO
+#define RT_HEAVY_PRIO 16
+#endif
+#ifndef RT_HEAVY_PRIO_LEVEL
+#define RT_HEAVY_PRIO_LEVEL 3
+#endif
 
 // The traversal loop. One iteration = one unit of this lane's work (expand a
 // node, test a leaf, or resume/pop a frame). (Measured and rejected: the
@@ -300,14 +309,20 @@ constexpr int kCoopRays = RT_COOP_RAYS;
 // of the wave are still looping, store the state and return true (suspended).
 template <int BLOCK, bool ANY, bool FAST, bool TAIL, uint32_t LB = RT_LEAF_BATCH, class CT>
 __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                         LdsStack<BLOCK> st, MState &S, CT &cnt, int coop_rays = kCoopRays) {
+                                         LdsStack<BLOCK> st, MState &S, CT &cnt, int coop_rays = kCoopRays,
+                                         int prio_iters = 0) {
   uint32_t word = S.word, flist = S.flist, fcnt = S.fcnt, fnode = S.fnode, cwnext = S.cwnext, gk = S.gk;
   float fbest = S.fbest, tnext = S.tnext, gbest = S.gbest;
   int depth = S.depth;
   bool have_t = S.have_t;
   bool suspended = false;
+  int it = 0;  // wave-uniform iteration count (prio_iters)
   for (;;) {
     if (TAIL && __popcll(__ballot(1)) <= coop_rays) { suspended = true; break; }
+    if (TAIL && prio_iters > 0) {
+      it = __builtin_amdgcn_readfirstlane(it + 1);
+      if (it == prio_iters) __builtin_amdgcn_s_setprio(RT_HEAVY_PRIO_LEVEL);
+    }
     if (word != rtl::kInvalidChild) {
       if (word & rtl::kLeafBit) {
         float lt = kInf;
@@ -586,7 +601,9 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
 template <int BLOCK>
 __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
                                                   bool active, uint32_t *stk_block, float &out_t,
-                                                  uint32_t &out_k, int coop_rays = kCoopRays) {
+                                                  uint32_t &out_k, int coop_rays = kCoopRays,
+                                                  int prio_iters = 0) {
+  if (prio_iters > 0) __builtin_amdgcn_s_setprio(0);  // a new tile starts at normal priority
   NoCnt cnt;
   const int lane = threadIdx.x & 63;
   LdsStack<BLOCK> st{stk_block + threadIdx.x};
@@ -613,9 +630,9 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   bool suspended = false;
   if (pending && sc.coop)
     suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
-                                                                                  coop_rays)
+                                                                                  coop_rays, prio_iters)
                      : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
-                                                                                   coop_rays);
+                                                                                   coop_rays, prio_iters);
   else if (pending)
     (void)(fast ? mesh_run<BLOCK, false, true, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
                 : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt));
