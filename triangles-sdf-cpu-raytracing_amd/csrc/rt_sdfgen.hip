@@ -233,13 +233,15 @@ int query_host(rt_sdf_mesh *m, const float *p3, int64_t n, float *out) {
   HIP_TRY(hipSetDevice(m->device));
   float *dp = nullptr, *dd = nullptr;
   int rc = RT_OK;
-  if (hipMalloc(&dp, (size_t)n * 12) != hipSuccess || hipMalloc(&dd, (size_t)n * 4) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, "hipMalloc failed for the query points");
-  } else if (hipMemcpy(dp, p3, (size_t)n * 12, hipMemcpyHostToDevice) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, "hipMemcpy H2D failed");
+  hipError_t e = hipSuccess;
+  if ((e = hipMalloc(&dp, (size_t)n * 12)) != hipSuccess || (e = hipMalloc(&dd, (size_t)n * 4)) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, std::string("hipMalloc failed for the query points: ") + hipGetErrorString(e));
+  } else if ((e = hipMemcpy(dp, p3, (size_t)n * 12, hipMemcpyHostToDevice)) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, std::string("hipMemcpy H2D failed: ") + hipGetErrorString(e) + " (" +
+                                     std::to_string(n) + " points)");
   } else if ((rc = query_device(m, dp, n, dd)) == RT_OK &&
-             hipMemcpy(out, dd, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, "hipMemcpy D2H failed");
+             (e = hipMemcpy(out, dd, (size_t)n * 4, hipMemcpyDeviceToHost)) != hipSuccess) {
+    rc = rterr::set(RT_E_DEVICE, std::string("hipMemcpy D2H failed: ") + hipGetErrorString(e));
   }
   if (dp) (void)hipFree(dp);
   if (dd) (void)hipFree(dd);
