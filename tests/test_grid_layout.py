@@ -93,17 +93,13 @@ def _batch_frames(gs, params, W, H):
 
 @pytest.mark.parametrize("size", [(103, 97, 130), (24, 24, 24), (65, 65, 65)])
 @pytest.mark.parametrize("mode", ["primary", "default"])
-def test_grid_lds_block_cache_frames(gpu, size, mode):
-    """The per-wave LDS block cache of the march (kGridLds, rtx_set_grid_lds):
-    multi-frame launches on the bricked (103x97x130) and linear (24^3, 65^3)
-    layouts equal the oracle's frames bit for bit, with the cache on and off,
-    including the default mode's shadow and reflection rays (which march
-    through the same cache)."""
-    import ctypes as C
+def test_grid_multi_frame_launches(gpu, size, mode):
+    """Multi-frame launches on the bricked (103x97x130) and linear (24^3,
+    65^3) layouts equal the oracle's frames bit for bit, including the default
+    mode's shadow and reflection rays. (Round 4 ran this with the per-wave LDS
+    block cache on and off; the cache was removed in round 5.)"""
     sz, vals = sdf_grid(size, zlib.crc32(repr(size).encode()) + 1)
     ref_s, gpu_s = cpuref.RefScene.grid(sz, vals), rtamd.SDFGrid(sz, vals)
-    L = rtamd.lib()
-    L.rtx_set_grid_lds.argtypes = [C.c_void_p, C.c_int]
     sm, plane = {"primary": (0, False), "default": (1, True)}[mode]
     ref_s.set_plane(plane, (0.0, 1.0, 0.0), -0.8)
     gpu_s.set_plane(rtamd.Plane((0.0, 1.0, 0.0), -0.8) if plane else None)
@@ -116,8 +112,6 @@ def test_grid_lds_block_cache_frames(gpu, size, mode):
         rp.append(cpuref.make_params(pos, vi, pi, (2, 2, 2), sm, True, True))
     refs = [ref_s.render(p, W, H)[:2] for p in rp]
     gpu_s.render(gp[0], np.zeros((H, W), np.uint32), np.full((H, W), np.inf, np.float32), clear=True)  # create
-    for on in (1, 0):
-        rtamd._lib.check(L.rtx_set_grid_lds(gpu_s._h, on))
-        for k, ((gc, gt), (rc, rt_)) in enumerate(zip(_batch_frames(gpu_s, gp, W, H), refs)):
-            assert np.array_equal(rc, gc), f"lds={on} {size} {mode} frame {k}: {(rc != gc).sum()} px differ"
-            assert np.array_equal(rt_.view(np.uint32), gt.view(np.uint32)), f"lds={on} {size} {mode} frame {k}: t"
+    for k, ((gc, gt), (rc, rt_)) in enumerate(zip(_batch_frames(gpu_s, gp, W, H), refs)):
+        assert np.array_equal(rc, gc), f"{size} {mode} frame {k}: {(rc != gc).sum()} px differ"
+        assert np.array_equal(rt_.view(np.uint32), gt.view(np.uint32)), f"{size} {mode} frame {k}: t"

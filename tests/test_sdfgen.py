@@ -93,8 +93,8 @@ def _points(name, n, seed):
 def test_sdf_points_bit_exact(gpu, rt, name, n):
     v, i = mesh(name)
     p = _points(name, n, 11)
-    m = rt.SDFMesh(rt.SimpleMesh(v, i))
-    got = m.points(p)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        got = m.points(p)
     ref = cpuref.sdf_points(v, i, p, 16)
     bad = np.flatnonzero(got.view(np.uint32) != ref.view(np.uint32))
     assert bad.size == 0, f"{bad.size} of {len(p)} differ, e.g. {p[bad[:3]]} {got[bad[:3]]} {ref[bad[:3]]}"
@@ -105,8 +105,8 @@ def test_sdf_points_bit_exact(gpu, rt, name, n):
                                        ("stanford-bunny.obj", (16, 16, 16))])
 def test_sdf_grid_bit_exact(gpu, rt, name, size):
     v, i = mesh(name)
-    m = rt.SDFMesh(rt.SimpleMesh(v, i))
-    sz, got = m.grid(size)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        sz, got = m.grid(size)
     ref = cpuref.sdf_points(v, i, cpuref.lattice_points(size), 16)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
@@ -115,8 +115,8 @@ def test_sdf_grid_bit_exact(gpu, rt, name, size):
 @pytest.mark.parametrize("name,depth", [("cube.obj", 4), ("spot.obj", 3), ("stanford-bunny.obj", 3)])
 def test_sdf_octree_bit_exact(gpu, rt, name, depth):
     v, i = mesh(name)
-    m = rt.SDFMesh(rt.SimpleMesh(v, i))
-    got = m.octree(depth)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        got = m.octree(depth)
     ref = cpuref.sdf_octree(v, i, depth, 16)
     assert got.size == ref.size and np.array_equal(got, ref)
 
@@ -128,8 +128,8 @@ def test_config3_standin_grid_sampled(gpu, rt):
     random lattice samples equal the oracle's brute force bit for bit, and the
     grid is a plausible SDF (negative inside, |grad| <= 1 between samples)."""
     v, i = mesh("stanford-bunny.obj")
-    m = rt.SDFMesh(rt.SimpleMesh(v, i))
-    size, vals = m.grid(256)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        size, vals = m.grid(256)
     assert vals.size == 256 ** 3
     rng = np.random.default_rng(3)
     idx = rng.integers(0, vals.size, 3000)
@@ -151,22 +151,48 @@ def test_render_generated_standins_bit_exact(gpu, rt, kind):
     """Frames of the GENERATED bunny SDF (grid 96^3 / octree depth 6) on the GPU
     equal the oracle's frames of the same data (primary and default mode)."""
     v, i = mesh("stanford-bunny.obj")
-    m = rt.SDFMesh(rt.SimpleMesh(v, i))
-    if kind == "grid":
-        size, vals = m.grid(96)
-        ref_s, gpu_s = cpuref.RefScene.grid(size, vals), rt.SDFGrid(size, vals)
-    else:
-        nodes = m.octree(6)
-        ref_s, gpu_s = cpuref.RefScene.octree(nodes), rt.SDFOctree(nodes)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        if kind == "grid":
+            size, vals = m.grid(96)
+            ref_s, gpu_s = cpuref.RefScene.grid(size, vals), rt.SDFGrid(size, vals)
+        else:
+            nodes = m.octree(6)
+            ref_s, gpu_s = cpuref.RefScene.octree(nodes), rt.SDFOctree(nodes)
     W, H = 320, 240
-    for mode, pos in (("primary", (0.0, 0.0, 2.5)), ("default", (1.5, 0.8, 2.0))):
-        plane = S.MODES[mode][1]
-        ref_s.set_plane(plane, (0.0, 1.0, 0.0), -1.0)
-        gpu_s.set_plane(rt.Plane((0.0, 1.0, 0.0), -1.0) if plane else None)
-        rc, rtt, _, _ = ref_s.render(S.params("stanford-bunny.obj", W, H, mode, pos, "ref"), W, H)
-        gc = np.zeros((H, W), np.uint32)
-        gt = np.full((H, W), np.inf, np.float32)
-        gpu_s.render(S.params("stanford-bunny.obj", W, H, mode, pos, "gpu"), gc, gt, clear=True)
-        assert np.isfinite(rtt).sum() > 1000
-        assert np.array_equal(rc, gc), f"{kind} {mode}: {(rc != gc).sum()} colour px differ"
-        assert np.array_equal(rtt.view(np.uint32), gt.view(np.uint32))
+    with gpu_s:
+        for mode, pos in (("primary", (0.0, 0.0, 2.5)), ("default", (1.5, 0.8, 2.0))):
+            plane = S.MODES[mode][1]
+            ref_s.set_plane(plane, (0.0, 1.0, 0.0), -1.0)
+            gpu_s.set_plane(rt.Plane((0.0, 1.0, 0.0), -1.0) if plane else None)
+            rc, rtt, _, _ = ref_s.render(S.params("stanford-bunny.obj", W, H, mode, pos, "ref"), W, H)
+            gc = np.zeros((H, W), np.uint32)
+            gt = np.full((H, W), np.inf, np.float32)
+            gpu_s.render(S.params("stanford-bunny.obj", W, H, mode, pos, "gpu"), gc, gt, clear=True)
+            assert np.isfinite(rtt).sum() > 1000
+            assert np.array_equal(rc, gc), f"{kind} {mode}: {(rc != gc).sum()} colour px differ"
+            assert np.array_equal(rtt.view(np.uint32), gt.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_stale_hip_error_reported_as_such(gpu, rt):
+    """A HIP error left pending by an earlier call (here librtamd's own
+    hipSetDevice(-1), rtx_inject_stale_error) is not taken for the failure of
+    the next query's copy: the query succeeds, bit-exact, and the stale error
+    is reported separately, naming the call that raised it (the round-4
+    'hipMemcpy H2D failed' could not tell the two apart)."""
+    import ctypes as C
+    L = rt.lib()
+    L.rtx_sdf_last_stale.restype = C.c_char_p
+    v, i = mesh("cube.obj")
+    p = _points("cube.obj", 500, 5)
+    ref = cpuref.sdf_points(v, i, p, 16)
+    with rt.SDFMesh(rt.SimpleMesh(v, i)) as m:
+        assert m.points(p).view(np.uint32).tolist() == ref.view(np.uint32).tolist()
+        assert L.rtx_sdf_last_stale() == b""
+        assert L.rtx_inject_stale_error() == 0
+        got = m.points(p)  # succeeds: the pending error is not this call's
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        msg = L.rtx_sdf_last_stale().decode()
+        assert "stale HIP error" in msg and "hipSetDevice(-1)" in msg, msg
+        m.points(p)
+        assert L.rtx_sdf_last_stale() == b""  # read and cleared once

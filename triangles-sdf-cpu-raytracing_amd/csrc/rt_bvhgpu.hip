@@ -869,12 +869,12 @@ struct PhaseTimer {
   hipStream_t st = nullptr;
   void start() {
     if (!on) return;
-    (void)hipStreamSynchronize(st);
+    HIP_NOTE(hipStreamSynchronize(st));
     t0 = std::chrono::steady_clock::now();
   }
   void stop(int k) {
     if (!on) return;
-    (void)hipStreamSynchronize(st);
+    HIP_NOTE(hipStreamSynchronize(st));
     acc[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
 };
@@ -886,7 +886,7 @@ struct DevArena {
   char *base = nullptr;
   size_t cap = 0, off = 0;
   ~DevArena() {
-    if (base) (void)hipFree(base);
+    if (base) HIP_NOTE(hipFree(base));
   }
   static size_t round(size_t b) { return (b + 255) & ~(size_t)255; }
   void *take(size_t bytes) {
@@ -904,7 +904,7 @@ struct DBuf {
   size_t cap = 0;
   bool owned = false;
   ~DBuf() {
-    if (p && owned) (void)hipFree(p);
+    if (p && owned) HIP_NOTE(hipFree(p));
   }
   static size_t first_cap(size_t n) { return std::max<size_t>(n, 1024); }  // what the first reserve(n) takes
   // grows geometrically: the per-stage buffers widen with the tree, and a
@@ -913,7 +913,7 @@ struct DBuf {
   int reserve(size_t n) {
     if (n <= cap) return RT_OK;
     const size_t want = std::max<size_t>({n, 2 * cap, 1024});
-    if (p && owned) (void)hipFree(p);
+    if (p && owned) HIP_NOTE(hipFree(p));
     p = nullptr;
     cap = 0;
     owned = false;
@@ -1157,7 +1157,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   pt.st = st;
   struct StreamGuard {
     hipStream_t s;
-    ~StreamGuard() { (void)hipStreamDestroy(s); }
+    ~StreamGuard() { HIP_NOTE(hipStreamDestroy(s)); }
   } sg{st};
   std::vector<uint32_t> iota(n);
   for (uint32_t t = 0; t < n; ++t) iota[t] = t;
@@ -1252,7 +1252,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     SG.advance();
   }
   if (pt.on) {
-    (void)hipStreamSynchronize(st);
+    HIP_NOTE(hipStreamSynchronize(st));
     pt.acc[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
   }
   pt.start();
@@ -1287,7 +1287,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
     BVH_DEV(hipMalloc(&tp, tbytes), "triangles");
     out.dev_tris.p = tp;
     out.dev_tris.bytes = tbytes;
-    out.dev_tris.release = [](void *q) { (void)hipFree(q); };
+    out.dev_tris.release = [](void *q) { HIP_NOTE(hipFree(q)); };
     BVH_DEV(hipMemsetAsync((rtl::GTri *)tp + out.n_tris, 0, 8 * sizeof(rtl::GTri), st), "triangles");
     if (nl) {
       if (dtab.reserve(3 * (size_t)nl)) return fail("allocation");
@@ -1379,7 +1379,7 @@ int rtx_sort_check(const float *keys, int64_t n, int32_t depth, uint32_t *ids_ou
               hipMemcpy(dev.data(), ids3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess ||
               hipMemcpy(dkv.data(), KV3.p, (size_t)nn * 4, hipMemcpyDeviceToHost) != hipSuccess))
     rc = rterr::set(RT_E_DEVICE, "download");
-  (void)hipStreamDestroy(S.st);
+  HIP_NOTE(hipStreamDestroy(S.st));
   if (rc) return rc;
   int64_t bad = 0;
   // a position counts once if its id differs from std::sort's or its carried

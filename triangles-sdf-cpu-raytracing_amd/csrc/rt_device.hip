@@ -34,6 +34,25 @@ int set(int code, const std::string &msg) {
   return code;
 }
 const char *get() { return g_err.c_str(); }
+thread_local std::string g_noted;
+thread_local hipError_t g_noted_err = hipSuccess;
+hipError_t note(const char *call, hipError_t e) {
+  if (e != hipSuccess) {
+    g_noted = call;
+    g_noted_err = e;
+  }
+  return e;
+}
+std::string take_stale() {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return {};
+  std::string m = std::string("stale HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) +
+                  ") was pending from an earlier call: ";
+  m += e == g_noted_err ? "librtamd's " + g_noted : std::string("a HIP call outside librtamd");
+  g_noted.clear();
+  g_noted_err = hipSuccess;
+  return m;
+}
 }  // namespace rterr
 
 namespace {
@@ -41,10 +60,6 @@ namespace {
 inline int set_err(int code, const std::string &msg) { return rterr::set(code, msg); }
 
 constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
-// Coop threshold of a persistent wave's last item (0: the same as every item's)
-#ifndef RT_TAIL_COOP
-#define RT_TAIL_COOP 0
-#endif
 // Workgroup of the persistent multi-frame kernel (render_persist_kernel), in
 // threads. Its waves are independent (each pulls its own items), so the block
 // only sets the granularity at which a launch's resources are handed back:
@@ -101,7 +116,6 @@ struct FrameArgs {
 #endif
 struct MeshS {
   static constexpr int kFields = 3;
-  static constexpr bool kWaveInit = false;
   static constexpr bool kCoop = true;  // primary rays: wave-cooperative tail (mesh_primary_wave)
   static constexpr int kMinWaves = RT_MESH_WAVES;
   static constexpr int kQueueGroup = 2;  // wave tiles per work-queue item (render_persist_kernel)
@@ -140,11 +154,7 @@ struct MeshS {
 };
 template <int kMode>
 struct GridS {
-  // no traversal stack (one unused LDS word per lane); with kGridLds the wave's
-  // LDS block cache: kFields words per lane, used as one contiguous region per
-  // wave (grid_lds_region)
-  static constexpr int kFields = (kMode & kGridLds) ? (kGridLdsWords + 63) / 64 : 1;
-  static constexpr bool kWaveInit = (kMode & kGridLds) != 0;  // the block cache's tags start empty
+  static constexpr int kFields = 1;  // no traversal stack (one unused LDS word per lane)
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_GRID_WAVES;
   // block dispatch: a grid tile is too short for the queue's claims to pay
@@ -152,29 +162,15 @@ struct GridS {
   static constexpr int kQueueGroup = 0;
   static constexpr int kLdsNodes = 0;
   GridDev d;
-  // the wave's contiguous kFields * 64 words of the block's stack array (the
-  // stack is lane-interleaved from stk + threadIdx.x; the grid has no stack)
-  template <int B>
-  __device__ __forceinline__ static float *grid_lds_region(LdsStack<B, kFields> st) {
-    uint32_t *blk = st.base - threadIdx.x;
-    return reinterpret_cast<float *>(blk + (threadIdx.x >> 6) * (kFields * 64));
-  }
-  // every lane of the wave, before its tile: the cache's 8 tags empty (LDS
-  // keeps the previous workgroup's words)
-  template <int B>
-  __device__ __forceinline__ static void wave_init(uint32_t *stk) {
-    uint32_t *region = stk + (threadIdx.x >> 6) * (kFields * 64);
-    if ((threadIdx.x & 63) < kGridLdsSlots) region[kGridLdsSlots * kGridLdsBlk + (threadIdx.x & 63)] = 0u;
-  }
   template <int B, class CT>
   __device__ __forceinline__ Hit intersect(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields> st, CT &cnt) const {
-    return grid_intersect<kMode>(d, o, dir, tn, tf, cnt, (kMode & kGridLds) ? grid_lds_region<B>(st) : nullptr);
+    return grid_intersect<kMode>(d, o, dir, tn, tf, cnt);
   }
   template <int B, class CT>
   __device__ __forceinline__ bool occluded(f3 o, f3 dir, float tn, float tf,
                                            LdsStack<B, kFields> st, CT &cnt) const {
-    return grid_occluded<kMode>(d, o, dir, tn, tf, cnt, (kMode & kGridLds) ? grid_lds_region<B>(st) : nullptr);
+    return grid_occluded<kMode>(d, o, dir, tn, tf, cnt);
   }
 };
 // PACK: the traversal carries the node coordinates packed in one register
@@ -182,7 +178,6 @@ struct GridS {
 template <bool PACK>
 struct OctS {
   static constexpr int kFields = kOctFields;
-  static constexpr bool kWaveInit = false;
   static constexpr bool kCoop = false;
   static constexpr int kMinWaves = RT_OCT_WAVES;
   static constexpr int kQueueGroup = 2;
@@ -386,7 +381,6 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
   const bool active = xo < fa.W && yl < fa.rows_local;
   // wave-cooperative primary path: every lane of the wave takes part
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
-  if constexpr (S::kWaveInit) S::template wave_init<B>(stk);  // (all lanes of the wave are here)
   if (DIAG == 0 && !kWaveCoop && !active) return false;
   if (active || kWaveCoop) {  // (the counting variant keeps every lane for its wave reduction)
     LdsStack<B, S::kFields> st{stk + threadIdx.x};
@@ -717,13 +711,6 @@ void render_persist_kernel(S sc_arg, PlaneDev pl, FrameBatch fb, PersistQ q) {
       k = knext;
       continue;
     }
-#if RT_TAIL_COOP
-    // the launch's tail: this wave's head has no item after this one, so the
-    // wave runs with few others and its heavy rays are issue-bound; hand its
-    // last RT_TAIL_COOP rays to 8-lane groups (rounds of 8) instead of 8
-    if constexpr (S::kCoop && !GENERAL)
-      sc.coop_rays = (q.cpf == 0 ? knext * 8 + h >= q.items : knext >= q.nper) ? RT_TAIL_COOP : kCoopRays;
-#endif
     const uint32_t ty = r / q.tiles_x, tx = r - ty * q.tiles_x;
 #ifdef RT_PERSIST_STAMPS
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1161,12 +1148,6 @@ struct rt_scene {
   uint32_t sched_grid = 0;
   bool sched_on = true;
   bool coop = true;  // mesh primary rays: cooperative tail (rtx_set_coop)
-  // grid: multi-frame launches march through the per-wave LDS block cache
-  // (kGridLds; rtx_set_grid_lds, RTAMD_GRID_LDS=1 for new scenes)
-  bool grid_lds = [] {
-    const char *e = std::getenv("RTAMD_GRID_LDS");
-    return e && e[0] == '1';
-  }();
   hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
   hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
@@ -1258,8 +1239,8 @@ int ensure_copy_streams(rt_scene *s) {
 
 int ensure_fb(rt_scene *s, size_t px) {
   if (px <= s->fb_cap) return RT_OK;
-  if (s->d_color) (void)hipFree(s->d_color);
-  if (s->d_t) (void)hipFree(s->d_t);
+  if (s->d_color) HIP_NOTE(hipFree(s->d_color));
+  if (s->d_t) HIP_NOTE(hipFree(s->d_t));
   s->d_color = nullptr;
   s->d_t = nullptr;
   s->fb_cap = 0;
@@ -1308,8 +1289,8 @@ int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStre
   if (!s->sched_on || !same_stream) return RT_OK;
   const uint32_t nb = gx * gy;
   if (nb > s->sched_cap) {
-    if (s->d_cost) (void)hipFree(s->d_cost);
-    if (s->d_order) (void)hipFree(s->d_order);
+    if (s->d_cost) HIP_NOTE(hipFree(s->d_cost));
+    if (s->d_order) HIP_NOTE(hipFree(s->d_order));
     s->d_cost = s->d_order = nullptr;
     s->sched_cap = 0;
     s->sched_grid = 0;
@@ -1409,7 +1390,7 @@ int stream_queue(hipStream_t stream, uint32_t **out) {
   HIP_TRY(hipMallocAsync(&p, kQueueBytes, stream));
   const hipError_t e = hipMemsetAsync(p, 0, kQueueBytes, stream);
   if (e != hipSuccess) {
-    (void)hipFreeAsync(p, stream);
+    HIP_NOTE(hipFreeAsync(p, stream));
     return set_err(RT_E_DEVICE, std::string("work-queue init: ") + hipGetErrorString(e));
   }
   g_queues[{dev, stream}] = (uint32_t *)p;
@@ -1559,7 +1540,7 @@ struct PumpOf<OctS<PK>> {
 };
 template <int kMode>
 struct PumpOf<GridS<kMode>> {
-  static constexpr bool kHas = (kMode & kGridLds) == 0;  // (the block cache is the tile kernels')
+  static constexpr bool kHas = true;
   using P = GridP<kMode>;
   static P make(const GridS<kMode> &s) { return P{s.d}; }
 };
@@ -1624,14 +1605,7 @@ int launch_batch(rt_scene *s, FrameBatch &fb, int n, hipStream_t stream) {
   } else if (s->kind == RT_SCENE_GRID) {
     const GridDev gd = grid_dev(s);
     const int mode = grid_mode(s, gd);
-    // the LDS block cache (rtx_set_grid_lds / RTAMD_GRID_LDS; A/B switch, buffer modes only)
-    switch ((s->grid_lds && (mode & kGridBuf)) ? (mode | kGridLds) : mode) {
-      case kGridBuf | kGridBricked | kGridLds:
-        rc = launch_batch_t<GridS<kGridBuf | kGridBricked | kGridLds>, 1>(s, {gd}, s->plane, fb, n, general, stream);
-        break;
-      case kGridBuf | kGridLds:
-        rc = launch_batch_t<GridS<kGridBuf | kGridLds>, 1>(s, {gd}, s->plane, fb, n, general, stream);
-        break;
+    switch (mode) {
       case kGridBuf | kGridBricked:
         rc = launch_batch_t<GridS<kGridBuf | kGridBricked>, 1>(s, {gd}, s->plane, fb, n, general, stream);
         break;
@@ -1731,7 +1705,7 @@ int build_bvh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t n
     // fails too, so the failure is reported here instead of at the upload
     if (const hipError_t e = hipDeviceSynchronize(); e != hipSuccess)
       return set_err(RT_E_DEVICE, err + "; device unusable afterwards: " + hipGetErrorString(e));
-    (void)hipGetLastError();
+    (void)hipGetLastError();  // the builder's failure was reported above: clear it
     std::fprintf(stderr, "rtamd: %s; building the BVH on the host instead\n", err.c_str());
     fell_back = true;
     err.clear();
@@ -1923,7 +1897,7 @@ int rt_scene_create_grid(const uint32_t size[3], const float *values, rt_scene *
   float *d_ref = nullptr;  // the reference array, staged for the device-side bricking
   if ((rc = upload(&d_ref, values, (size_t)n, s->dev_bytes)) ||
       (rc = upload(&s->d_vals, (const float *)nullptr, (size_t)nb, s->dev_bytes))) {
-    if (d_ref) (void)hipFree(d_ref);
+    if (d_ref) HIP_NOTE(hipFree(d_ref));
     rt_scene_destroy(s);
     return rc;
   }
@@ -2002,21 +1976,26 @@ int rt_scene_bvh_stats(const rt_scene *s, int64_t *nodes, int64_t *inner, int32_
 int rt_scene_destroy(rt_scene *s) {
   if (!s) return RT_OK;
   int prev = 0;
-  (void)hipGetDevice(&prev);
-  (void)hipSetDevice(s->device);
+  HIP_NOTE(hipGetDevice(&prev));
+  HIP_NOTE(hipSetDevice(s->device));
+  // the scene's own copy/render streams drain before anything they may still
+  // read or write is freed (rt_render returns only after both, but a failed
+  // call or a caller-stream launch may not have)
+  for (hipStream_t x : s->xs)
+    if (x) HIP_NOTE(hipStreamSynchronize(x));
   void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t,
                   s->d_cost, s->d_order};
   for (void *p : ptrs)
-    if (p) (void)hipFree(p);
-  if (s->sched_ev) (void)hipEventDestroy(s->sched_ev);
-  if (s->ev0) (void)hipEventDestroy(s->ev0);
-  if (s->ev1) (void)hipEventDestroy(s->ev1);
-  if (s->xev) (void)hipEventDestroy(s->xev);
-  if (s->d_hit_box) (void)hipFree(s->d_hit_box);
-  if (s->h_hit_box) (void)hipHostFree(s->h_hit_box);
+    if (p) HIP_NOTE(hipFree(p));
+  if (s->sched_ev) HIP_NOTE(hipEventDestroy(s->sched_ev));
+  if (s->ev0) HIP_NOTE(hipEventDestroy(s->ev0));
+  if (s->ev1) HIP_NOTE(hipEventDestroy(s->ev1));
+  if (s->xev) HIP_NOTE(hipEventDestroy(s->xev));
+  if (s->d_hit_box) HIP_NOTE(hipFree(s->d_hit_box));
+  if (s->h_hit_box) HIP_NOTE(hipHostFree(s->h_hit_box));
   for (hipStream_t x : s->xs)
-    if (x) (void)hipStreamDestroy(x);
-  (void)hipSetDevice(prev);
+    if (x) HIP_NOTE(hipStreamDestroy(x));
+  HIP_NOTE(hipSetDevice(prev));
   delete s;
   return RT_OK;
 }
@@ -2265,7 +2244,7 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
   auto cleanup = [&]() {
     void *ps[] = {dO, dD, dT, dN, dH, dP};
     for (void *q : ps)
-      if (q) (void)hipFree(q);
+      if (q) HIP_NOTE(hipFree(q));
   };
   hipError_t e = hipSuccess;
   do {
@@ -2325,7 +2304,7 @@ int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, i
   unsigned long long *d = nullptr;
   HIP_TRY(hipMalloc(&d, C_NUM * sizeof(unsigned long long)));
   hipError_t e = hipMemset(d, 0, C_NUM * sizeof(unsigned long long));
-  if (e == hipSuccess) (void)hipMemset(s->d_t, 0x7f, px * 4);
+  if (e == hipSuccess) HIP_NOTE(hipMemset(s->d_t, 0x7f, px * 4));
   for (int32_t f = 0; f < frames && e == hipSuccess && rc == RT_OK; ++f) {
     FrameArgs fa;
     if (!(rc = check_params(params + f, W, H)) &&
@@ -2334,7 +2313,7 @@ int rt_count_work(rt_scene *s, const rt_render_params *params, int32_t frames, i
   }
   unsigned long long h[C_NUM] = {};
   if (e == hipSuccess && rc == RT_OK) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  HIP_NOTE(hipFree(d));
   if (rc) return rc;
   if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rt_count_work: ") + hipGetErrorString(e));
   for (int i = 0; i < C_NUM; ++i) counters[i] = (int64_t)h[i];
@@ -2359,7 +2338,7 @@ int rtx_wave_stamps(rt_scene *s, const rt_render_params *params, int32_t W, int3
   if (!(rc = fill_frame(fa, params, s->d_color, s->d_t, W, H, flags, nullptr)))
     rc = launch_render(s, fa, 0, d, 2);
   hipError_t e = rc ? hipSuccess : hipMemcpy(out, d, nw * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  HIP_NOTE(hipFree(d));
   if (rc) return rc;
   if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
   *nwaves = nw;
@@ -2434,7 +2413,7 @@ int rtx_eye_rays(const rt_render_params *p, int32_t W, int32_t H, float *out) {
   eye_rays_kernel<<<(W * H + 255) / 256, 256>>>(*p, W, H, d);
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)W * H * 12, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  HIP_NOTE(hipFree(d));
   if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
   return RT_OK;
 }
@@ -2460,7 +2439,7 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
   if (e == hipSuccess) e = hipMemcpy(mt, dmt, (size_t)n * 4, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(mk, dmk, (size_t)n * 4, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(orv, dor, (size_t)n * 4, hipMemcpyDeviceToHost);
-  for (void *q : {(void *)dk, (void *)dst, (void *)dsid, (void *)dmt, (void *)dmk, (void *)dor}) (void)hipFree(q);
+  for (void *q : {(void *)dk, (void *)dst, (void *)dsid, (void *)dmt, (void *)dmk, (void *)dor}) HIP_NOTE(hipFree(q));
   if (e != hipSuccess) return set_err(RT_E_DEVICE, hipGetErrorString(e));
   return RT_OK;
 }
@@ -2502,11 +2481,6 @@ int rtx_set_coop(rt_scene *s, int on) {
 
 // Diagnostic switch: primary-ray batches of this scene on the ray pump
 // (render_pump_kernel) instead of one tile per wave (default off).
-int rtx_set_grid_lds(rt_scene *s, int on) {
-  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
-  s->grid_lds = on != 0;
-  return RT_OK;
-}
 
 int rtx_set_pump(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");

@@ -767,25 +767,11 @@ struct GridDev {
 __host__ __device__ __forceinline__ uint32_t grid_bricks(uint32_t n) { return (n + kBrick - 1) / kBrick; }
 
 // grid kernel modes: bit 0 = buffer loads with 32-bit byte offsets (else 64-bit
-// addresses), bit 1 = bricked (else linear), bit 2 = the march's taps through
-// the per-wave LDS block cache (grid_lds_taps; with bit 0 only). Separate kernel
-// instantiations, so the rare 64-bit path does not set the common one's
-// register budget.
-constexpr int kGridBuf = 1, kGridBricked = 2, kGridLds = 4;
-
-// Per-wave LDS block cache of the sphere march (kGridLds, north star: "SDF-voxel
-// tiles staged through LDS"). A slot holds the 5x5x5 samples [4b, 4b+4]^3 of a
-// 4x4x4 brick b and its +1 halo, so every tap of a cell whose c0 lies in b is
-// in the slot (c1 <= c0 + 1). Slots are direct-mapped by the brick's parity
-// bits (bx & 1, by & 1, bz & 1: the 8 bricks around any point go to 8
-// different slots). A march step whose cell changed looks its block up; the
-// wave serves the distinct blocks its lanes need one at a time (wave-uniform
-// loop): a missing block is loaded by all active lanes together (125 samples,
-// ~2 loads per lane) into its slot, then the lanes of that block read their
-// 8 taps from LDS. Same samples, same bits as the buffer loads.
-constexpr int kGridLdsSlots = 8;
-constexpr int kGridLdsBlk = 128;  // floats per slot (125 used)
-constexpr int kGridLdsWords = kGridLdsSlots * kGridLdsBlk + kGridLdsSlots;  // + one tag per slot
+// addresses), bit 1 = bricked (else linear). Separate kernel instantiations,
+// so the rare 64-bit path does not set the common one's register budget.
+// (A per-wave LDS block cache of the march was built in round 4 and measured
+// 2.8-5x slower; it was removed in round 5)
+constexpr int kGridBuf = 1, kGridBricked = 2;
 
 // a * b for sample offsets. In buffer mode both factors are below 2^24
 // (grid_mode checks the strides) and the product below 2^30 (a sample
@@ -853,63 +839,9 @@ __device__ __forceinline__ void grid_fetch(const GridDev &g, uint32_t i0x, uint3
   }
 }
 
-// The 8 taps of cell (i0, i1) through the wave's LDS block cache (kGridLds).
-// lds = this wave's kGridLdsWords words (blocks, then the 8 tags: brick id + 1).
-template <int kMode>
-__device__ __forceinline__ void grid_lds_taps(const GridDev &g, float *lds, uint32_t i0x, uint32_t i0y, uint32_t i0z,
-                                              uint32_t i1x, uint32_t i1y, uint32_t i1z, float v[8]) {
-  constexpr int kM = kMode & ~kGridLds;
-  uint32_t *tags = reinterpret_cast<uint32_t *>(lds + kGridLdsSlots * kGridLdsBlk);
-  const uint32_t bx = i0x >> 2, by = i0y >> 2, bz = i0z >> 2;
-  const uint32_t nby = grid_bricks(g.sy), nbz = grid_bricks(g.sz);
-  const uint32_t key = (bx * nby + by) * nbz + bz + 1u;
-  const uint32_t slot = (bx & 1u) * 4u + (by & 1u) * 2u + (bz & 1u);
-  // the lane's tap offsets inside its block
-  const uint32_t b0 = (i0x - 4u * bx) * 25u + (i0y - 4u * by) * 5u + (i0z - 4u * bz);
-  const uint32_t dx = (i1x - i0x) * 25u, dy = (i1y - i0y) * 5u, dz = i1z - i0z;
-  bool pending = true;
-  for (;;) {  // one distinct block per iteration, wave-uniform
-    const uint64_t need = __ballot(pending);
-    if (need == 0) break;
-    const int leader = (int)__builtin_ctzll(need);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
-    const uint32_t sl = __builtin_amdgcn_readlane(slot, leader);
-    float *blk = lds + sl * kGridLdsBlk;
-    if (tags[sl] != k) {  // miss: the active lanes load the block together
-      const uint32_t kb = k - 1u, lbz = kb % nbz, lby = (kb / nbz) % nby, lbx = kb / nbz / nby;
-      const uint64_t act = __ballot(1);
-      const uint32_t nact = (uint32_t)__popcll(act);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-      for (uint32_t i = rank; i < 125u; i += nact) {
-        const uint32_t sx = 4u * lbx + i / 25u, sy = 4u * lby + (i / 5u) % 5u, sz = 4u * lbz + i % 5u;
-        if (sx < g.sx && sy < g.sy && sz < g.sz) {  // (samples past the grid are never a tap)
-          const uint32_t o = grid_ox<kM>(g, sx) + grid_oy<kM>(g, sy) + grid_oz<kM>(sz);
-          const __amdgpu_buffer_rsrc_t r =
-              __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.v), 0, (int)g.bytes, kBufWord3);
-          blk[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, o << 2, 0, 0));
-        }
-      }
-      if (rank == 0) tags[sl] = k;
-    }
-    if (pending && key == k) {
-      v[0] = blk[b0];
-      v[1] = blk[b0 + dz];
-      v[2] = blk[b0 + dy];
-      v[3] = blk[b0 + dy + dz];
-      v[4] = blk[b0 + dx];
-      v[5] = blk[b0 + dx + dz];
-      v[6] = blk[b0 + dx + dy];
-      v[7] = blk[b0 + dx + dy + dz];
-      pending = false;
-    }
-  }
-}
-
 // SDFGrid::sdf(float3) (grid_raytracing.cpp:7-62). CACHE: taps from / into tc.
-// kGridLds: lds = this wave's block cache (else unused).
 template <int kMode, bool CACHE, class CT>
-__device__ __forceinline__ float grid_sdf_t(const GridDev &g, f3 p, uint32_t *cell, GridTaps &tc, CT &cnt,
-                                            float *lds = nullptr) {
+__device__ __forceinline__ float grid_sdf_t(const GridDev &g, f3 p, uint32_t *cell, GridTaps &tc, CT &cnt) {
   cnt.add(C_GRID_SDF, 1);
   p = f3{(p.x + 1.0f) / 2.0f, (p.y + 1.0f) / 2.0f, (p.z + 1.0f) / 2.0f};
   p = p * f3{(float)(g.sx - 1), (float)(g.sy - 1), (float)(g.sz - 1)};
@@ -925,16 +857,13 @@ __device__ __forceinline__ float grid_sdf_t(const GridDev &g, f3 p, uint32_t *ce
   float v[8];
   if constexpr (CACHE) {
     if (!(i0x == tc.i0x && i0y == tc.i0y && i0z == tc.i0z && i1x == tc.i1x && i1y == tc.i1y && i1z == tc.i1z)) {
-      if constexpr ((kMode & kGridLds) != 0)
-        grid_lds_taps<kMode>(g, lds, i0x, i0y, i0z, i1x, i1y, i1z, tc.v);
-      else
-        grid_fetch<kMode>(g, i0x, i0y, i0z, i1x, i1y, i1z, tc.v);
+      grid_fetch<kMode>(g, i0x, i0y, i0z, i1x, i1y, i1z, tc.v);
       tc.i0x = i0x; tc.i0y = i0y; tc.i0z = i0z; tc.i1x = i1x; tc.i1y = i1y; tc.i1z = i1z;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = tc.v[k];
   } else {
-    grid_fetch<kMode & ~kGridLds>(g, i0x, i0y, i0z, i1x, i1y, i1z, v);
+    grid_fetch<kMode>(g, i0x, i0y, i0z, i1x, i1y, i1z, v);
   }
   float res = 0.0f;
   res += v[0] * bx * by * bz;
@@ -980,10 +909,9 @@ __device__ __forceinline__ f3 grid_normal(const GridDev &g, f3 p, CT &cnt) {  //
 enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 
 // grid_raytracing.cpp:93-125. Returns hit and leaves the hit point in *hp.
-// kGridLds: lds = this wave's block cache.
 template <int kMode, class CT>
 __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
-                                           float &out_t, f3 &hp, uint32_t &cell, CT &cnt, float *lds = nullptr) {
+                                           float &out_t, f3 &hp, uint32_t &cell, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   float t1, t2;
   bbox_intersection(f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, inv, tNear, tFar, t1, t2);
@@ -994,7 +922,7 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
   GridTaps tc;
   while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
-    const float s = grid_sdf_t<kMode, RT_GRID_TAP_CACHE != 0 || (kMode & kGridLds) != 0>(g, p, &cell, tc, cnt, lds);
+    const float s = grid_sdf_t<kMode, RT_GRID_TAP_CACHE != 0>(g, p, &cell, tc, cnt);
     if (s < 1e-3f) {
       out_t = t + s;
       hp = p;
@@ -1008,13 +936,13 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
 
 template <int kMode, class CT>
 __device__ __forceinline__ Hit grid_intersect(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
-                                              CT &cnt, float *lds = nullptr) {
+                                              CT &cnt) {
   Hit h = miss_hit();
   f3 p;
   uint32_t cell;
-  if (grid_march<kMode>(g, o, d, tNear, tFar, h.t, p, cell, cnt, lds)) {
+  if (grid_march<kMode>(g, o, d, tNear, tFar, h.t, p, cell, cnt)) {
     h.hit = true;
-    h.n = grid_normal<kMode & ~kGridLds>(g, p, cnt);  // the normal's 6 evaluations load their taps
+    h.n = grid_normal<kMode>(g, p, cnt);  // the normal's 6 evaluations load their taps
     h.prim = (int64_t)cell;
   } else {
     h.t = kInf;
@@ -1023,11 +951,11 @@ __device__ __forceinline__ Hit grid_intersect(const GridDev &g, f3 o, f3 d, floa
 }
 template <int kMode, class CT>
 __device__ __forceinline__ bool grid_occluded(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
-                                              CT &cnt, float *lds = nullptr) {
+                                              CT &cnt) {
   float t;
   f3 p;
   uint32_t cell;
-  return grid_march<kMode>(g, o, d, tNear, tFar, t, p, cell, cnt, lds);
+  return grid_march<kMode>(g, o, d, tNear, tFar, t, p, cell, cnt);
 }
 
 // SDFGrid::intersect (grid_raytracing.cpp:93-125) split for the ray pump

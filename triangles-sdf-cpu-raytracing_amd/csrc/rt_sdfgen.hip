@@ -37,11 +37,18 @@ struct rt_sdf_mesh {
   int device = 0;
   int32_t oct_depth = -1;          // octree cache (two-call protocol of rt_sdf_mesh_octree)
   std::vector<uint8_t> oct_nodes;
+  // point queries: the handle's own non-blocking stream, and pinned host /
+  // device staging for up to q_cap points, reused across calls
+  hipStream_t qs = nullptr;
+  float *h_stage = nullptr;  // q_cap * 4 floats: points (3 per point), then distances
+  float *d_p3 = nullptr, *d_out = nullptr;
+  int64_t q_cap = 0;
 };
 
 namespace {
 
 constexpr int kWave = 64;
+thread_local std::string g_stale_seen;  // the last stale error a query found (rtx_sdf_last_stale)
 
 struct SdfDev {
   const rtl::GNode *nodes;
@@ -216,36 +223,73 @@ SdfDev dev_of(const rt_sdf_mesh *m) { return SdfDev{m->d_nodes, m->d_tri, m->d_p
 
 size_t lds_bytes(const rt_sdf_mesh *m) { return (size_t)m->stack_cap * kWave * 8; }
 
-// Evaluate n points (device buffers) on the null stream and wait.
-int query_device(rt_sdf_mesh *m, const float *d_p3, int64_t n, float *d_out) {
-  if (n <= 0) return RT_OK;
-  const int64_t blocks = (n + kWave - 1) / kWave;
-  if (blocks > 0x7FFFFFFF) return rterr::set(RT_E_INVALID, "too many points");
-  hipLaunchKernelGGL(sdf_kernel<false>, dim3((uint32_t)blocks), dim3(kWave), lds_bytes(m), 0, dev_of(m), d_p3,
-                     n, 0u, 0u, 0u, m->stack_cap, d_out);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
+// Points per staged batch of a host query (16 MiB of pinned staging at most).
+constexpr int64_t kQueryBatch = 1 << 20;
+
+// The handle's query stream and staging for batches of up to `n` points.
+int query_staging(rt_sdf_mesh *m, int64_t n) {
+  if (!m->qs) HIP_TRY(hipStreamCreateWithFlags(&m->qs, hipStreamNonBlocking));
+  const int64_t want = std::min(n, kQueryBatch);
+  if (want <= m->q_cap) return RT_OK;
+  HIP_TRY(hipStreamSynchronize(m->qs));
+  if (m->h_stage) HIP_NOTE(hipHostFree(m->h_stage));
+  if (m->d_p3) HIP_NOTE(hipFree(m->d_p3));
+  if (m->d_out) HIP_NOTE(hipFree(m->d_out));
+  m->h_stage = m->d_p3 = m->d_out = nullptr;
+  m->q_cap = 0;
+  const int64_t cap = std::max<int64_t>(want, 4096);
+  HIP_TRY(hipHostMalloc(&m->h_stage, (size_t)cap * 16, hipHostMallocDefault));
+  HIP_TRY(hipMalloc(&m->d_p3, (size_t)cap * 12));
+  HIP_TRY(hipMalloc(&m->d_out, (size_t)cap * 4));
+  m->q_cap = cap;
   return RT_OK;
 }
 
+// Signed distances of n host points. Every copy goes between the handle's
+// pinned staging and device buffers on its own stream, so no pageable
+// transfer (HIP's internal staging or on-the-fly pinning of caller memory)
+// is on this path; each step reports its own failure, and an error that was
+// already pending before the first copy is reported as such
+// (rterr::take_stale) -- round 4 saw one "hipMemcpy H2D failed" here that
+// carried no HIP error string.
 int query_host(rt_sdf_mesh *m, const float *p3, int64_t n, float *out) {
   if (n <= 0) return RT_OK;
+  const std::string stale = rterr::take_stale();  // before any call of ours can overwrite it
+  g_stale_seen = stale;
   HIP_TRY(hipSetDevice(m->device));
-  float *dp = nullptr, *dd = nullptr;
-  int rc = RT_OK;
-  hipError_t e = hipSuccess;
-  if ((e = hipMalloc(&dp, (size_t)n * 12)) != hipSuccess || (e = hipMalloc(&dd, (size_t)n * 4)) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, std::string("hipMalloc failed for the query points: ") + hipGetErrorString(e));
-  } else if ((e = hipMemcpy(dp, p3, (size_t)n * 12, hipMemcpyHostToDevice)) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, std::string("hipMemcpy H2D failed: ") + hipGetErrorString(e) + " (" +
-                                     std::to_string(n) + " points)");
-  } else if ((rc = query_device(m, dp, n, dd)) == RT_OK &&
-             (e = hipMemcpy(out, dd, (size_t)n * 4, hipMemcpyDeviceToHost)) != hipSuccess) {
-    rc = rterr::set(RT_E_DEVICE, std::string("hipMemcpy D2H failed: ") + hipGetErrorString(e));
+  if (const hipError_t e = hipStreamQuery(m->qs ? m->qs : nullptr); e != hipSuccess && e != hipErrorNotReady)
+    return rterr::set(RT_E_DEVICE, std::string("device already in error before the SDF query: ") +
+                                       hipGetErrorString(e) + (stale.empty() ? "" : "; " + stale));
+  int rc = query_staging(m, n);
+  if (rc != RT_OK) return rc;
+  for (int64_t i0 = 0; i0 < n; i0 += m->q_cap) {
+    const int64_t k = std::min(m->q_cap, n - i0);
+    std::memcpy(m->h_stage, p3 + 3 * i0, (size_t)k * 12);
+    hipError_t e = hipMemcpyAsync(m->d_p3, m->h_stage, (size_t)k * 12, hipMemcpyHostToDevice, m->qs);
+    const char *step = "hipMemcpyAsync H2D of the points";
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(sdf_kernel<false>, dim3((uint32_t)((k + kWave - 1) / kWave)), dim3(kWave), lds_bytes(m),
+                         m->qs, dev_of(m), m->d_p3, k, 0u, 0u, 0u, m->stack_cap, m->d_out);
+      e = hipGetLastError();
+      step = "sdf_kernel launch";
+    }
+    float *h_out = m->h_stage + 3 * m->q_cap;
+    if (e == hipSuccess) {
+      e = hipMemcpyAsync(h_out, m->d_out, (size_t)k * 4, hipMemcpyDeviceToHost, m->qs);
+      step = "hipMemcpyAsync D2H of the distances";
+    }
+    if (e == hipSuccess) {
+      e = hipStreamSynchronize(m->qs);
+      step = "hipStreamSynchronize after the query";
+    }
+    if (e != hipSuccess) {
+      HIP_NOTE(hipStreamSynchronize(m->qs));
+      return rterr::set(RT_E_DEVICE, std::string("SDF query of ") + std::to_string(k) + " points: " + step +
+                                         ": " + hipGetErrorString(e) + (stale.empty() ? "" : "; " + stale));
+    }
+    std::memcpy(out + i0, h_out, (size_t)k * 4);
   }
-  if (dp) (void)hipFree(dp);
-  if (dd) (void)hipFree(dd);
-  return rc;
+  return RT_OK;
 }
 
 bool octree_query(void *ctx, const float *p3, int64_t n, float *out, std::string &err) {
@@ -302,6 +346,7 @@ int rt_sdf_mesh_grid(rt_sdf_mesh *m, const uint32_t size[3], float *values) {
   const int64_t n = (int64_t)size[0] * size[1] * size[2];
   const uint64_t blocks = (uint64_t)((size[0] + 3) / 4) * ((size[1] + 3) / 4) * ((size[2] + 3) / 4);
   if (blocks > 0x7FFFFFFFull) return rterr::set(RT_E_INVALID, "grid too large");
+  g_stale_seen = rterr::take_stale();
   HIP_TRY(hipSetDevice(m->device));
   float *d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)n * 4));
@@ -310,7 +355,7 @@ int rt_sdf_mesh_grid(rt_sdf_mesh *m, const uint32_t size[3], float *values) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(values, d, (size_t)n * 4, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  HIP_NOTE(hipFree(d));
   if (e != hipSuccess) return rterr::set(RT_E_DEVICE, std::string("sdf grid: ") + hipGetErrorString(e));
   return RT_OK;
 }
@@ -336,9 +381,17 @@ int rt_sdf_mesh_octree(rt_sdf_mesh *m, int32_t depth, int64_t *count, void *node
 
 int rt_sdf_mesh_destroy(rt_sdf_mesh *m) {
   if (!m) return RT_OK;
-  if (m->d_nodes) (void)hipFree(m->d_nodes);
-  if (m->d_tri) (void)hipFree(m->d_tri);
-  if (m->d_pn) (void)hipFree(m->d_pn);
+  HIP_NOTE(hipSetDevice(m->device));
+  if (m->qs) {
+    HIP_NOTE(hipStreamSynchronize(m->qs));
+    HIP_NOTE(hipStreamDestroy(m->qs));
+  }
+  if (m->h_stage) HIP_NOTE(hipHostFree(m->h_stage));
+  if (m->d_p3) HIP_NOTE(hipFree(m->d_p3));
+  if (m->d_out) HIP_NOTE(hipFree(m->d_out));
+  if (m->d_nodes) HIP_NOTE(hipFree(m->d_nodes));
+  if (m->d_tri) HIP_NOTE(hipFree(m->d_tri));
+  if (m->d_pn) HIP_NOTE(hipFree(m->d_pn));
   delete m;
   return RT_OK;
 }
@@ -361,5 +414,14 @@ int rt_mesh_subdivide(const float *vpos4, int64_t nverts, const uint32_t *idx, i
   *out_nidx = ni;
   return RT_OK;
 }
+
+// Test hooks: leave a HIP error pending on this thread through a librtamd
+// call (hipSetDevice(-1)), and read the stale error the last SDF call of this
+// thread found before its first copy ("" if none).
+int rtx_inject_stale_error(void) {
+  HIP_NOTE(hipSetDevice(-1));
+  return RT_OK;
+}
+const char *rtx_sdf_last_stale(void) { return g_stale_seen.c_str(); }
 
 }  // extern "C"

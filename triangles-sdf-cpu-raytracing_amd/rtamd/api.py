@@ -336,8 +336,14 @@ class IScene:
 
     def close(self):
         if self._h is not None:
-            lib().rt_scene_destroy(self._h)
+            check(lib().rt_scene_destroy(self._h))
             self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def __del__(self):
         try:
@@ -456,8 +462,14 @@ class SDFMesh:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().rt_sdf_mesh_destroy(self._h)
+            check(lib().rt_sdf_mesh_destroy(self._h))
             self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def __del__(self):
         try:
