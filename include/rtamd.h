@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 6
+#define RTAMD_ABI_VERSION 7
 
 enum rt_status {
   RT_OK = 0,
@@ -152,6 +152,15 @@ int64_t rt_scene_device_bytes(const rt_scene *s);
 /* Statistics of the host BVH (mesh scenes): node count, inner count, max depth. */
 int rt_scene_bvh_stats(const rt_scene *s, int64_t *nodes, int64_t *inner, int32_t *max_depth);
 int rt_scene_destroy(rt_scene *s);
+/* A copy of scene s on another HIP device (device arrays copied device to
+ * device, over xGMI between GPUs; no rebuild): the same tree, plane and kernel
+ * instantiation, so every frame it renders is bitwise s's. For replicating one
+ * scene on the GPUs of a single-process multi-GPU render (rt_multi_create). */
+int rt_scene_replicate(const rt_scene *s, int device, rt_scene **out);
+/* HIP device the scene lives on. */
+int rt_scene_device(const rt_scene *s);
+/* The plane last given to rt_scene_set_plane (enabled, normal, offset). */
+int rt_scene_get_plane(const rt_scene *s, int *enabled, float normal[3], float *offset);
 
 /* ---- frames ------------------------------------------------------------- */
 /* Renderer::draw on HOST buffers color[W*H] (RGBA8 packed, R in the low byte)
@@ -204,6 +213,42 @@ int rt_clear_device(uint32_t *d_color, float *d_t, int64_t n, void *stream);
  * counterpart: the reference renders on the host (src/raytracing.cpp:67-102). */
 int rt_stream_prepare(void *stream);
 int rt_stream_release(void *stream);
+
+/* ---- multi-GPU rendering in ONE process (Renderer::draw over n devices) --
+ * The reference renders a frame with one call, Renderer::draw (src/main.cpp:
+ * 196-207), which splits it by image rows across OpenMP threads
+ * (src/raytracing.cpp:77-96). rt_multi does the same across GPUs of one
+ * process: the scene (on devices[0], the root) is replicated on every other
+ * device (rt_scene_replicate), the frame is cut into bands of band_rows rows,
+ * band b -> slot b mod n (rt_tile), every slot renders its bands packed on its
+ * own stream, and the bands come to the root in one gather per frame and
+ * buffer: RCCL ncclGather over a communicator from ncclCommInitAll when the
+ * devices are distinct, device-to-device (peer) copies when a device is
+ * listed more than once (RCCL refuses a device twice in one communicator; the
+ * one-GPU test box runs {0, 0}). The root de-interleaves them
+ * (rt_untile_device). Frames are bitwise the single-device frames. */
+typedef struct rt_multi rt_multi;
+enum rt_multi_exchange { RT_MULTI_RCCL = 1, RT_MULTI_PEER_COPY = 2 };
+/* scene must live on devices[0]; it is not owned and must outlive the handle
+ * (its plane is re-read at every render). band_rows <= 0 selects 8. */
+int rt_multi_create(rt_scene *scene, const int32_t *devices, int32_t n, int32_t band_rows, rt_multi **out);
+/* Slots, the exchange in use (rt_multi_exchange) and the band height. */
+int rt_multi_info(const rt_multi *m, int32_t *n, int32_t *exchange, int32_t *band_rows);
+/* Renderer::draw on HOST buffers, the same contract as rt_render (flags 0 =
+ * tPrev frame, RT_FLAG_CLEAR, RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY). Blocks until
+ * the assembled frame is in color / t. *ms (optional): device time from the
+ * first launch to the assembled frame on the root (HIP events). */
+int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
+                    uint32_t flags, float *ms);
+/* `frames` frames into DEVICE buffers on the root (d_color[f], d_t[f]),
+ * flags must contain RT_FLAG_CLEAR. Stream-ordered on `stream` (a stream of
+ * the root device, or NULL): the slots start after the work queued on it so
+ * far, and it waits for the assembled frames; the host does not block. Each
+ * slot renders up to 16 frames per launch (rt_render_device_frames). */
+int rt_multi_render_device_frames(rt_multi *m, const rt_render_params *params, int32_t frames,
+                                  uint32_t *const *d_color, float *const *d_t, int32_t W, int32_t H,
+                                  uint32_t flags, void *stream);
+int rt_multi_destroy(rt_multi *m);
 
 /* ---- frame exchange over xGMI (multi-GPU, one process per GPU) -----------
  * Rank 0 allocates its frame slots with rt_exchange_alloc, exports them with

@@ -230,3 +230,42 @@ def _oracle_frame(key, W, H, mode, k):
     rs, _ = scenes(key)
     set_plane(key, mode, rs, scenes(key)[1])
     return rs.render(S.params(key, W, H, mode, orbit_positions(64)[k], "ref"), W, H)
+
+
+@pytest.mark.parametrize("devices", [(0, 0), (0,)], ids=["peer_copy_0_0", "rccl_0"])
+@pytest.mark.parametrize("mode", ["primary", "default"])
+def test_config5_single_process_multi_device(gpu, devices, mode):
+    """configs[4] through the single-process multi-GPU surface (rt_multi, the
+    C ABI a C++ Renderer::draw binds): the 1,111,216-triangle stand-in at
+    3840x2160, rendered over `devices` -- (0, 0) is two slots on the one GPU
+    of the test box, gathered by peer copies; (0,) is one slot gathered by
+    RCCL's ncclGather through an ncclCommInitAll communicator -- into the
+    caller's host buffers, and through the device-frames entry the bench
+    times. Every assembled frame is bitwise the oracle's whole frame."""
+    import torch
+
+    import rtamd
+    from rtamd.workloads import orbit_positions
+    W, H = CASES["mesh_large"]
+    rs, gs = scenes("mesh_large")
+    set_plane("mesh_large", mode, rs, gs)
+    k = 37
+    P = S.params("mesh_large", W, H, mode, orbit_positions(64)[k], "gpu")
+    c, t, _, _ = _oracle_frame("mesh_large", W, H, mode, k)
+    with rtamd.MultiRenderer(gs, devices, band_rows=8) as mr:
+        n, exch, br = mr.info()
+        assert (n, br) == (len(devices), 8)
+        assert exch == (mr.PEER_COPY if len(set(devices)) < len(devices) else mr.RCCL)
+        gc = np.zeros((H, W), np.uint32)
+        gt = np.full((H, W), np.inf, np.float32)
+        mr.render(P, gc, gt, cleared=True)
+        assert_same((c, t), (gc, gt), f"rt_multi_render {devices} {mode}")
+        cs = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        ts = [torch.empty((H, W), dtype=torch.float32, device="cuda") for _ in range(2)]
+        st = torch.cuda.current_stream()
+        P2 = S.params("mesh_large", W, H, mode, orbit_positions(64)[5], "gpu")
+        mr.render_device_frames([P2, P], [x.data_ptr() for x in cs], [x.data_ptr() for x in ts], W, H,
+                                stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert_same((c, t), (cs[1].cpu().numpy().view(np.uint32), ts[1].cpu().numpy()),
+                    f"rt_multi_render_device_frames {devices} {mode}")

@@ -26,4 +26,12 @@ else
   /opt/rocm/bin/hipcc $HIPF $2 -c -o build/var/rt_device_$1.o $SRC
   DEV=build/var/rt_device_$1.o BVH=build/rt_bvhgpu.o
 fi
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/var_$1.so build/rt_host.o build/rt_bvhstage.o build/rt_meshops.o $DEV build/rt_sdfgen.o $BVH build/rt_buildid.o -lgomp
+# the variant's own build id: the tree's id + its name and a hash of its
+# flags and revision, so a bench line from a variant never passes for the
+# shipping library's
+make -s build/rt_buildid.o
+BASE=$(sed -n 's/.*return "\([0-9a-f]*\)".*/\1/p' build/rt_buildid.cpp)
+VH=$(printf '%s|%s|%s|%s' "$2" "$3" "$VAR_UNIT" "$HIPF" | sha256sum | cut -c1-8)
+printf 'extern "C" const char *rt_build_id(void) { return "%s+%s:%s"; }\n' "$BASE" "$1" "$VH" > build/var/rt_buildid_$1.cpp
+g++ -fPIC -c -o build/var/rt_buildid_$1.o build/var/rt_buildid_$1.cpp
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/var_$1.so build/rt_host.o build/rt_bvhstage.o build/rt_meshops.o $DEV build/rt_sdfgen.o $BVH build/rt_multi.o build/var/rt_buildid_$1.o -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

@@ -1935,6 +1935,66 @@ int rt_scene_create_octree(const void *nodes36, int64_t count, rt_scene **out) {
   return RT_OK;
 }
 
+int rt_scene_replicate(const rt_scene *src, int device, rt_scene **out) {
+  if (!src || !out) return set_err(RT_E_INVALID, "bad arguments");
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return set_err(RT_E_INVALID, "rt_scene_replicate: no such device");
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(device));
+  rt_scene *s = new rt_scene();
+  // the scene's description (kind, tree shape, plane, kernel instantiation)
+  s->kind = src->kind;
+  s->device = device;
+  s->maxd = src->maxd;
+  s->root = src->root;
+  std::memcpy(s->root_box, src->root_box, sizeof s->root_box);
+  s->host_nodes = src->host_nodes;
+  s->host_inner = src->host_inner;
+  s->n_inner = src->n_inner;
+  s->bvh_depth = src->bvh_depth;
+  std::memcpy(s->size, src->size, sizeof s->size);
+  s->grid_bricked = src->grid_bricked;
+  s->oct_depth = src->oct_depth;
+  s->plane = src->plane;
+  s->dev_bytes = src->dev_bytes;
+  s->sched_on = src->sched_on;
+  s->coop = src->coop;
+  s->pump_on = src->pump_on;
+  // the device arrays, copied device to device (over xGMI between GPUs)
+  void *const from[] = {src->d_nodes, src->d_tris, src->d_vals, src->d_child, src->d_ovals};
+  void **to[] = {(void **)&s->d_nodes, (void **)&s->d_tris, (void **)&s->d_vals, (void **)&s->d_child,
+                 (void **)&s->d_ovals};
+  hipError_t e = hipSuccess;
+  const char *step = "";
+  for (int i = 0; i < 5 && e == hipSuccess; ++i) {
+    if (!from[i]) continue;
+    size_t bytes = 0;
+    if ((e = hipMemPtrGetInfo(from[i], &bytes)) != hipSuccess) { step = "hipMemPtrGetInfo"; break; }
+    if ((e = hipMalloc(to[i], bytes)) != hipSuccess) { step = "hipMalloc"; break; }
+    if ((e = hipMemcpyPeer(*to[i], device, from[i], src->device, bytes)) != hipSuccess) step = "hipMemcpyPeer";
+  }
+  HIP_NOTE(hipSetDevice(prev));
+  if (e != hipSuccess) {
+    rt_scene_destroy(s);
+    return set_err(RT_E_DEVICE, std::string("rt_scene_replicate: ") + step + ": " + hipGetErrorString(e));
+  }
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_device(const rt_scene *s) { return s ? s->device : RT_E_INVALID; }
+
+int rt_scene_get_plane(const rt_scene *s, int *enabled, float normal[3], float *offset) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  if (enabled) *enabled = s->plane.on;
+  if (normal) { normal[0] = s->plane.n.x; normal[1] = s->plane.n.y; normal[2] = s->plane.n.z; }
+  if (offset) *offset = s->plane.off;
+  return RT_OK;
+}
+
 int rt_scene_set_plane(rt_scene *s, int enabled, const float normal[3], float offset) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   PlaneDev &p = s->plane;

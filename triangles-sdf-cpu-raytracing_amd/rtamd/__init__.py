@@ -5,7 +5,7 @@ reference's shading) runs in hand-written HIP kernels in librtamd.so; this
 package only marshals arguments.
 """
 from ._lib import EXPORTED, LIB_PATH, RT_FLAG_CLEAR, RenderParams, RtError, Tile, build, lib
-from .api import (BVHBuilder, Camera, FrameBuffer, HitInfo, IScene, Plane, Renderer, SceneUnion,
+from .api import (BVHBuilder, Camera, FrameBuffer, HitInfo, IScene, MultiRenderer, Plane, Renderer, SceneUnion,
                   SDFGrid, SDFMesh, SDFOctree, ShadingMode, SimpleMesh, camera_matrices, device_count,
                   load_mesh_from_obj, load_sdf_grid, load_sdf_octree, render_params, save_mesh_to_obj,
                   subdivide_mesh)
@@ -13,7 +13,7 @@ from . import data, tiles, workloads
 
 __all__ = [
     "EXPORTED", "LIB_PATH", "RT_FLAG_CLEAR", "RenderParams", "RtError", "Tile", "build", "lib",
-    "BVHBuilder", "Camera", "FrameBuffer", "HitInfo", "IScene", "Plane", "Renderer", "SceneUnion",
+    "BVHBuilder", "Camera", "FrameBuffer", "HitInfo", "IScene", "MultiRenderer", "Plane", "Renderer", "SceneUnion",
     "SDFGrid", "SDFMesh", "SDFOctree", "ShadingMode", "SimpleMesh", "camera_matrices", "device_count",
     "load_mesh_from_obj", "load_sdf_grid", "load_sdf_octree", "render_params", "save_mesh_to_obj",
     "subdivide_mesh",

@@ -79,6 +79,16 @@ _SIGS = {
     "rt_scene_bvh_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int32)]),
     "rt_scene_destroy": (C.c_int, [C.c_void_p]),
+    "rt_scene_replicate": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_scene_device": (C.c_int, [C.c_void_p]),
+    "rt_scene_get_plane": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.POINTER(C.c_float)]),
+    "rt_multi_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_multi_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rt_multi_render": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                  C.c_uint32, C.POINTER(C.c_float)]),
+    "rt_multi_render_device_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                                C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
+    "rt_multi_destroy": (C.c_int, [C.c_void_p]),
     "rt_render": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                             C.c_uint32, C.POINTER(C.c_float)]),
     "rt_host_pin": (C.c_int, [C.c_void_p, C.c_int64]),
@@ -131,13 +141,15 @@ EXPORTED = tuple(_SIGS)
 def source_build_id() -> str:
     """rt_build_id() of a library built from this tree (the Makefile's ID_SRCS
     rule): sha256 of csrc/{*.cpp,*.h,*.hip} in sorted order, then
-    include/rtamd.h; first 16 hex digits."""
+    include/rtamd.h, then the Makefile (its compile flags); first 16 hex
+    digits. Variant builds (tools/build_variant.sh) append "+<name>:<flags
+    hash>", so they never pass for the shipping library."""
     import glob
     import hashlib
     srcs = sorted(os.path.relpath(p, PKG_ROOT) for ext in ("cpp", "h", "hip")
                   for p in glob.glob(os.path.join(PKG_ROOT, "csrc", f"*.{ext}")))
     h = hashlib.sha256()
-    for rel in srcs + [os.path.join("..", "include", "rtamd.h")]:
+    for rel in srcs + [os.path.join("..", "include", "rtamd.h"), "Makefile"]:
         with open(os.path.join(PKG_ROOT, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

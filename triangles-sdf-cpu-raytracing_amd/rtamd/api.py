@@ -30,6 +30,7 @@ __all__ = [
     "BVHBuilder", "SDFGrid", "SDFOctree", "Plane", "SceneUnion", "load_mesh_from_obj",
     "load_sdf_grid", "load_sdf_octree", "camera_matrices", "render_params", "RtError",
     "RT_FLAG_CLEAR", "Tile", "device_count", "SDFMesh", "subdivide_mesh", "save_mesh_to_obj",
+    "MultiRenderer",
 ]
 
 
@@ -423,6 +424,70 @@ class Renderer:
         P = render_params(camera.position(), camera.view_inv(), proj_inv, self.lightPos,
                           self.shadingMode, self.enableShadows, self.enableReflections)
         return base.render(P, frame_buffer.color, frame_buffer.t, clear=False)
+
+
+# ------------------------------------ one process, several GPUs (rt_multi) --
+class MultiRenderer:
+    """Renderer::draw over several GPUs of one process (rt_multi_*): the
+    scene (on devices[0]) is replicated on the other devices, the frame is cut
+    into row bands (band b -> slot b mod n, as the reference's draw splits rows
+    over OpenMP threads, raytracing.cpp:77-96), each slot renders its bands on
+    its own stream and one gather per frame (RCCL ncclGather for distinct
+    devices, peer copies when a device repeats) assembles it on devices[0]."""
+
+    RCCL, PEER_COPY = 1, 2
+
+    def __init__(self, scene: IScene, devices, band_rows: int = 8):
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        check(lib().rt_multi_create(scene._handle(), devs, len(devices), int(band_rows), C.byref(h)))
+        self._h = h
+        self.scene = scene  # the root scene must outlive the handle
+
+    def info(self):
+        """-> (slots, exchange (MultiRenderer.RCCL / PEER_COPY), band_rows)."""
+        n, x, b = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        check(lib().rt_multi_info(self._h, C.byref(n), C.byref(x), C.byref(b)))
+        return n.value, x.value, b.value
+
+    def render(self, params: RenderParams, color: np.ndarray, t: np.ndarray, clear: bool = False,
+               cleared: bool = False) -> float:
+        """The same contract as IScene.render (host buffers); returns the device
+        time from the first launch to the assembled frame, in ms."""
+        H, W = color.shape
+        assert color.dtype == np.uint32 and t.dtype == np.float32 and t.shape == color.shape
+        assert color.flags.c_contiguous and t.flags.c_contiguous
+        ms = C.c_float(0.0)
+        flags = (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) if cleared else RT_FLAG_CLEAR if clear else 0
+        check(lib().rt_multi_render(self._h, C.byref(params), _p(color), _p(t), W, H, flags, C.byref(ms)))
+        return ms.value
+
+    def render_device_frames(self, params_list, color_ptrs, t_ptrs, W: int, H: int,
+                             stream: int | None = None):
+        """Frames into device buffers on devices[0], stream-ordered on `stream`."""
+        n = len(params_list)
+        arr = (RenderParams * n)(*params_list)
+        cp = (C.c_void_p * n)(*color_ptrs)
+        tp = (C.c_void_p * n)(*t_ptrs)
+        check(lib().rt_multi_render_device_frames(self._h, arr, n, cp, tp, W, H, RT_FLAG_CLEAR,
+                                                  C.c_void_p(stream) if stream else None))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            check(lib().rt_multi_destroy(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # --------------------------------------------- mesh -> SDF (SURVEY 8(f) 1) --
