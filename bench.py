@@ -143,6 +143,12 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="file for the raw counters and per-launch times (not the JSON line)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N GPUs from ONE process (rt_multi: scene replicas, row bands, RCCL ncclGather)")
+    ap.add_argument("--devices", default=None,
+                    help="--single-process: comma-separated device list (default 0..N-1; a device may repeat)")
+    ap.add_argument("--no-single-process-leg", action="store_true",
+                    help="N>1: skip rank 0's single-process measurement over all N devices")
     ap.add_argument("--dist", action="store_true",
                     help="use the banded + gather path even at WORLD_SIZE 1 (protocol test)")
     return ap.parse_args()
@@ -618,6 +624,114 @@ def cpu_baseline(entry, budget_s, max_frames):
             "sample": f"{frames} orbit frames, {src} {W}x{H} {mode}"}, why
 
 
+def run_multi(scene, params, warmup, steps, W, H, devices, band_rows):
+    """One process, len(devices) slots (rt_multi): every frame split into row
+    bands over the devices and gathered on devices[0] (RCCL ncclGather, or peer
+    copies when a device repeats). The K timed frames go out as ONE
+    rt_multi_render_device_frames call (16 frames per slot launch, chunks
+    pipelined inside the library) into K resident frames on devices[0].
+    Returns (wall_s, exchange name, buffers of the last frame)."""
+    dev = torch.device("cuda", devices[0])
+    mr = rtamd.MultiRenderer(scene, devices, band_rows)
+    try:
+        n, exch, _ = mr.info()
+        st = stream_pool(1)[0]
+        nwarm = max(warmup, 16)
+        wb = [(torch.empty((H, W), dtype=torch.int32, device=dev), torch.empty((H, W), dtype=torch.float32, device=dev))
+              for _ in range(min(nwarm, 16))]
+        ob = [(torch.empty((H, W), dtype=torch.int32, device=dev), torch.empty((H, W), dtype=torch.float32, device=dev))
+              for _ in range(steps)]
+        for k0 in range(0, nwarm, len(wb)):
+            m = min(len(wb), nwarm - k0)
+            mr.render_device_frames([params[(k0 + i) % len(params)] for i in range(m)],
+                                    [c.data_ptr() for c, _ in wb[:m]], [t.data_ptr() for _, t in wb[:m]], W, H,
+                                    stream=st.cuda_stream)
+
+        def sync_all():
+            for d in sorted(set(devices)):
+                torch.cuda.synchronize(d)
+        gc.collect()
+        gc.disable()
+        try:
+            sync_all()
+            t0 = time.perf_counter()
+            mr.render_device_frames(params[warmup:warmup + steps], [c.data_ptr() for c, _ in ob],
+                                    [t.data_ptr() for _, t in ob], W, H, stream=st.cuda_stream)
+            sync_all()
+            wall = time.perf_counter() - t0
+        finally:
+            gc.enable()
+        return wall, ("rccl_gather" if exch == mr.RCCL else "peer_copy"), ob[-1]
+    finally:
+        mr.close()
+
+
+def single_process_main(a, json_out):
+    """bench.py --gpus N --single-process: the headline over N GPUs of ONE
+    process (the C ABI a C++ Renderer::draw binds, rt_multi_*)."""
+    key, entry = workload_entry(a.workload)
+    src, W, H, mode, cfg, desc = entry
+    devices = [int(x) for x in a.devices.split(",")] if a.devices else list(range(a.gpus))
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py needs a HIP device (the renderer has no CPU path)")
+    if max(devices) >= ndev:
+        raise SystemExit(f"bench.py --single-process: devices {devices} but {ndev} visible")
+    torch.cuda.set_device(devices[0])
+    rtamd._lib.check(rtamd.lib().rt_set_device(devices[0]))
+    scene, off = WL.scene_for(src)
+    scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
+    params = orbit_params(max(a.warmup + a.steps, 16), W, H, mode)
+    wall, exch, (lc, lt) = run_multi(scene, params, a.warmup, a.steps, W, H, devices, a.band_rows)
+    k = a.warmup + a.steps - 1
+    _, _, (c1, t1) = run_single(scene, params[k:k + 1], 0, 1, W, H, inflight=1)
+    ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
+    ms_step = wall * 1e3 / a.steps
+    algo, _ = work_model(scene, params[a.warmup:a.warmup + min(a.steps, 64)], None, W, H)
+    out = {
+        "metric": METRIC, "value": round(W * H * a.steps / wall / 1e6, 1), "unit": "Mrays/s",
+        "n_gpus": len(set(devices)), "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic deterministic 64-frame camera orbit over {desc}",
+        "config": {"workload": f"{key}: {desc}, {W}x{H}, "
+                               f"{'primary rays (Normal shading, no plane)' if mode == 'primary' else 'default shading'}"
+                               f" (BASELINE {cfg})",
+                   "resolution": [W, H], "camera": "orbit r=2.5 h=0.5 fovy 45",
+                   "parallelism": f"one process, {len(devices)} slots on devices {devices}, row bands of "
+                                  f"{a.band_rows} rows, exchange {exch} (rt_multi)"},
+        "roofline": roofline(algo, ms_step, scene.device_bytes(), None, "skipped (single-process leg)"),
+        "frame_check": {"last_timed_frame_equals_one_frame_kernel": ok},
+        "exchange": exch, "slots": len(devices),
+        "build_id": rtamd.lib().rt_build_id().decode(),
+    }
+    scene.close()
+    print(json.dumps(out, separators=(",", ":")), file=json_out, flush=True)
+    return 0 if ok else 1
+
+
+def single_process_leg(a, world):
+    """N>1, rank 0, after the ranks have left: the same workload over all N
+    devices from ONE child process (bench.py --single-process), so the
+    driver's multi-GPU run also measures the single-process C-ABI path."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--single-process",
+           "--steps", str(a.steps), "--warmup", str(a.warmup), "--workload", a.workload,
+           "--band-rows", str(a.band_rows)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc {r.returncode}: {(r.stderr or '')[-300:]}"}
+    o = json.loads(lines[-1])
+    return {"value": o["value"], "ms_per_step": o["ms_per_step"], "exchange": o["exchange"],
+            "slots": o["slots"], "frame_check": o["frame_check"], "parallelism": o["config"]["parallelism"]}
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -667,20 +781,35 @@ def spawn_ranks(n, json_out, grace_s=60.0, cmd=None, ndev=None):
                 sys.stderr.write(s)
     th = threading.Thread(target=relay, daemon=True)
     th.start()
-    failed_at = None
-    while any(p.poll() is None for p in procs):
-        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
-            failed_at = time.monotonic()
-        if failed_at is not None and time.monotonic() - failed_at > grace_s:
-            for p in procs:
-                if p.poll() is None:
-                    print(f"bench.py: killing rank {procs.index(p)} (a peer failed {grace_s:.0f} s ago)",
-                          file=sys.stderr)
-                    try:
-                        os.killpg(p.pid, signal.SIGKILL)
-                    except ProcessLookupError:
-                        pass
-        time.sleep(0.2)
+
+    def kill_all(why):
+        for p in procs:
+            if p.poll() is None:
+                print(f"bench.py: killing rank {procs.index(p)} ({why})", file=sys.stderr)
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+    # the ranks run in sessions of their own (a timeout's signal to our process
+    # group does not reach them), so a SIGTERM / SIGINT to this parent kills
+    # every rank still running before it exits, and so does any exception
+    def on_signal(signum, _frame):
+        kill_all(f"parent got signal {signum}")
+        raise SystemExit(128 + signum)
+    old = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        failed_at = None
+        while any(p.poll() is None for p in procs):
+            if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+                failed_at = time.monotonic()
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                kill_all(f"a peer failed {grace_s:.0f} s ago")
+            time.sleep(0.2)
+    finally:
+        kill_all("parent exiting")
+        for sig, h in old.items():
+            signal.signal(sig, h)
     th.join(timeout=10)
     rcs = [p.wait() for p in procs]
     rc = max((abs(x) for x in rcs), default=0)
@@ -708,6 +837,8 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     key, entry = workload_entry(a.workload)
     src, W, H, mode, cfg, desc = entry
+    if a.single_process:
+        sys.exit(single_process_main(a, json_out))
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(spawn_ranks(a.gpus, json_out))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -845,6 +976,12 @@ def main():
                 if k != key:
                     cb[k], _ = cpu_baseline(WORKLOADS[k], a.cpu_seconds * s, mx)
         out["cpu_baseline"] = cb
+    if use_dist:
+        dist.barrier()
+        sp_leg = (rank == 0 and not a.no_single_process_leg and dist.get_backend() == "nccl" and ndev >= world)
+        dist.destroy_process_group()
+        if sp_leg:  # the other ranks exit now; their GPUs are free for the child
+            out["single_process"] = single_process_leg(a, world)
     if rank == 0:
         try:
             os.makedirs(os.path.dirname(a.detail), exist_ok=True)
@@ -856,9 +993,6 @@ def main():
         line = json.dumps(out, separators=(",", ":"))
         print(f"bench line: {len(line)} bytes", file=sys.stderr, flush=True)
         print(line, file=json_out, flush=True)
-    if use_dist:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -255,6 +255,15 @@ struct Renderer {
   bool enableShadows = true;
   bool enableReflections = true;
   ShadingMode shadingMode = ShadingMode::Lambert;
+  // GPUs a frame is split over (one process; rt_multi_*): empty renders on the
+  // scene's device with rt_render. Otherwise the scene (which must live on
+  // devices[0]) is replicated on the others at the first draw, each device
+  // renders every n-th band of bandRows rows (the reference's draw splits
+  // rows over OpenMP threads, raytracing.cpp:77-96), and one gather per frame
+  // (RCCL ncclGather; peer copies when a device repeats) assembles it on
+  // devices[0]. The frame is bitwise the single-device frame.
+  std::vector<int32_t> devices;
+  int32_t bandRows = 8;
 
   // Renderer::draw: t is read as tPrev, pixels written only on hit
   // (raytracing.cpp:67-102). Returns the kernel time in milliseconds.
@@ -279,10 +288,35 @@ struct Renderer {
     p.enable_shadows = enableShadows;
     p.enable_reflections = enableReflections;
     float ms = 0.0f;
+    if (!devices.empty()) {
+      check(rt_multi_render(multi(scene), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
+                            (int32_t)fb.height(), 0u, &ms));
+      return ms;
+    }
     check(rt_render(scene.handle(), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
                     (int32_t)fb.height(), 0u, &ms));
     return ms;
   }
+  // the multi-GPU handle of (scene, devices, bandRows), made at first use
+  rt_multi *multi(const IScene &scene) const {
+    if (!multi_ || multi_scene_ != scene.handle() || multi_devices_ != devices || multi_rows_ != bandRows) {
+      multi_.reset();
+      rt_multi *m = nullptr;
+      check(rt_multi_create(scene.handle(), devices.data(), (int32_t)devices.size(), bandRows, &m));
+      multi_.reset(m, MultiDel{});
+      multi_scene_ = scene.handle();
+      multi_devices_ = devices;
+      multi_rows_ = bandRows;
+    }
+    return multi_.get();
+  }
+  struct MultiDel {
+    void operator()(rt_multi *m) const { rt_multi_destroy(m); }
+  };
+  mutable std::shared_ptr<rt_multi> multi_;
+  mutable const rt_scene *multi_scene_ = nullptr;
+  mutable std::vector<int32_t> multi_devices_;
+  mutable int32_t multi_rows_ = 0;
 };
 
 }  // namespace rtamd

@@ -68,3 +68,61 @@ def test_gloo_ranks_may_share_gpus(tmp_path, monkeypatch):
     monkeypatch.setenv("RTAMD_DIST_BACKEND", "gloo")
     rc, out = _run(tmp_path, "ok", n=2, ndev=1)
     assert rc == 0 and json.loads(out)["world"] == 2
+
+
+PARENT_SCRIPT = textwrap.dedent("""
+    import io, sys
+    sys.path.insert(0, sys.argv[1])
+    import bench
+    sys.exit(bench.spawn_ranks(2, io.StringIO(), cmd=[sys.executable, sys.argv[2]], ndev=2))
+""")
+
+SLEEP_RANK = textwrap.dedent("""
+    import os, sys, time
+    d = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(d, f"pid_{os.environ['RANK']}"), "w") as f:
+        f.write(str(os.getpid()))
+    time.sleep(600)
+""")
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    try:  # a zombie (exited, not yet reaped) counts as gone
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGINT"])
+def test_spawn_parent_signal_kills_every_rank(tmp_path, sig, monkeypatch):
+    """The ranks run in sessions of their own, so a timeout's signal to the
+    parent's process group never reaches them: the parent itself must kill
+    every rank still running when it is told to stop."""
+    import signal
+    import subprocess
+    import time
+    monkeypatch.delenv("RTAMD_DIST_BACKEND", raising=False)
+    (tmp_path / "parent.py").write_text(PARENT_SCRIPT)
+    (tmp_path / "rank.py").write_text(SLEEP_RANK)
+    p = subprocess.Popen([sys.executable, str(tmp_path / "parent.py"), ROOT, str(tmp_path / "rank.py")])
+    try:
+        t0 = time.monotonic()
+        while not all((tmp_path / f"pid_{r}").exists() for r in range(2)):
+            assert time.monotonic() - t0 < 120 and p.poll() is None, "ranks did not start"
+            time.sleep(0.1)
+        pids = [int((tmp_path / f"pid_{r}").read_text()) for r in range(2)]
+        assert all(_alive(q) for q in pids)
+        p.send_signal(getattr(signal, sig))
+        assert p.wait(timeout=60) != 0
+        t0 = time.monotonic()
+        while any(_alive(q) for q in pids) and time.monotonic() - t0 < 20:
+            time.sleep(0.1)
+        assert not any(_alive(q) for q in pids), "a rank outlived its parent"
+    finally:
+        if p.poll() is None:
+            p.kill()

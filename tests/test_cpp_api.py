@@ -82,3 +82,19 @@ def test_cli_save_obj_matches_reference_writer(rt, ref, tmp_path):
                    capture_output=True, text=True, timeout=120)
     v, i = ref.load_obj(data.path("cube.obj"))
     assert out.read_bytes() == ref.save_obj_text(v, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,W,H,mode", [GOLDEN_CASES[2], GOLDEN_CASES[4]])
+@pytest.mark.parametrize("devices", ["0,0", "0"])
+def test_cli_multi_device_reproduces_golden_hash(gpu, name, W, H, mode, devices):
+    """The C++ Renderer over several devices of one process (Renderer::devices
+    -> rt_multi_*, `rt_render --devices`): the same golden frames. On the
+    one-GPU box "0,0" is two slots gathered by peer copies, "0" one slot
+    gathered by RCCL."""
+    args = [CLI, data.path(name), "--size", str(W), str(H), "--frames", "2", "--devices", devices]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["devices"] == len(devices.split(","))
+    assert out["hash"] == S.GOLDEN[(name, W, H, mode)]

@@ -11,6 +11,8 @@
 //             [--plane 0|1] [--shadows 0|1] [--reflections 0|1] [--frames N]
 //             [--ppm out.ppm] [--png out.png] [--drag dx dy] [--zoom notches]
 //             [--save-obj out.obj]   (the loaded, scaled mesh via SaveMeshToObj)
+//             [--devices d0,d1,...] [--band-rows R]  (one process, several GPUs:
+//                                     Renderer::devices, rt_multi_*)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -44,7 +46,8 @@ int usage() {
                "usage: rt_render <input.obj|.grid|.octree> [--size W H] [--pos x y z]\n"
                "       [--mode normal|lambert|color] [--plane 0|1] [--shadows 0|1]\n"
                "       [--reflections 0|1] [--frames N] [--ppm out.ppm] [--png out.png]\n"
-               "       [--drag dx dy] [--zoom notches] [--save-obj out.obj]\n");
+               "       [--drag dx dy] [--zoom notches] [--save-obj out.obj]\n"
+               "       [--devices d0,d1,...] [--band-rows R]\n");
   return 2;
 }
 
@@ -109,6 +112,18 @@ int main(int argc, char **argv) {
     } else if (a == "--zoom") {  // mouse-wheel notches
       need(1);
       zoom = std::strtof(argv[++i], nullptr);
+    } else if (a == "--devices") {  // e.g. 0,1,2,3 (a device may repeat: 0,0)
+      need(1);
+      renderer.devices.clear();
+      for (const char *q = argv[++i]; *q;) {
+        char *end = nullptr;
+        renderer.devices.push_back((int32_t)std::strtol(q, &end, 10));
+        if (end == q) return usage();
+        q = *end == ',' ? end + 1 : end;
+      }
+    } else if (a == "--band-rows") {
+      need(1);
+      renderer.bandRows = std::atoi(argv[++i]);
     } else {
       return usage();
     }
@@ -116,6 +131,7 @@ int main(int argc, char **argv) {
   if (W == 0 || H == 0) return usage();
 
   try {
+    if (!renderer.devices.empty()) rtamd::check(rt_set_device(renderer.devices[0]));  // the scene lives on devices[0]
     std::unique_ptr<rtamd::IScene> scene;
     float planeY = -1.0f;  // SDF model box is [-1,1]^3 (main.cpp:176-184)
     if (ends_with(input, ".obj")) {
@@ -162,8 +178,9 @@ int main(int argc, char **argv) {
     if (png) fb.savePNG(png);
     std::printf(
         "{\"input\": \"%s\", \"width\": %u, \"height\": %u, \"frames\": %d, \"hash\": \"%016llx\", "
-        "\"covered\": %lld, \"kernel_ms\": %.4f}\n",
-        input.c_str(), W, H, frames, (unsigned long long)h, (long long)covered, total_ms / frames);
+        "\"covered\": %lld, \"kernel_ms\": %.4f, \"devices\": %zu}\n",
+        input.c_str(), W, H, frames, (unsigned long long)h, (long long)covered, total_ms / frames,
+        std::max<size_t>(renderer.devices.size(), 1));
     return 0;
   } catch (const std::exception &e) {
     std::fprintf(stderr, "%s\n", e.what());

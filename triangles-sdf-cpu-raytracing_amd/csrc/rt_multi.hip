@@ -59,6 +59,7 @@ struct rt_multi {
   std::vector<hipStream_t> st;    // per slot, on its device
   std::vector<hipEvent_t> done;   // per slot: its bands have left for the root
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // root: first launch .. assembled frame
+  hipEvent_t rc_free = nullptr;  // root: the last untile has read the receive buffers (peer copies wait)
   bool rccl = false;
   std::vector<ncclComm_t> comm;  // per slot (RCCL exchange)
   // buffers for frames of W x H, up to fcap frames per chunk
@@ -162,9 +163,11 @@ int exchange(rt_multi *m, int32_t k) {
     NCCL_TRY(ncclGroupEnd());
     return RT_OK;
   }
-  // peer copies: slot 0 rendered straight into the root's receive slots
+  // peer copies: slot 0 rendered straight into the root's receive slots; the
+  // other slots write them only after the root's previous untile read them
   for (int32_t i = 1; i < n; ++i) {
     HIP_TRY(hipSetDevice(m->dev[i]));
+    HIP_TRY(hipStreamWaitEvent(m->st[i], m->rc_free, 0));
     for (int32_t f = 0; f < k; ++f) {
       const size_t at = ((size_t)f * n + i) * cap;
       HIP_TRY(hipMemcpyPeerAsync(m->rc + at, m->dev[0], m->pc[i] + f * cap, m->dev[i], cap * 4, m->st[i]));
@@ -185,15 +188,18 @@ float *slot_t(rt_multi *m, int32_t i, int32_t f) {
   return (!m->rccl && i == 0) ? m->rt + (size_t)f * m->n * m->cap : m->pt[i] + (size_t)f * m->cap;
 }
 
-// Render frames params[0..k) on every slot (after ev0 on st[0]), exchange,
-// and untile frame f into out_c[f] / out_t[f] on the root's stream st[0].
+// Render frames params[0..k) on every slot (the slots first wait for ev0 when
+// `wait`), exchange, and untile frame f into out_c[f] / out_t[f] on the
+// root's stream st[0]. Chunks of one call need no wait between them: a slot's
+// next render follows its previous send on its own stream, and the root's
+// next gather follows its previous untile on st[0].
 int render_chunk(rt_multi *m, const rt_render_params *params, int32_t k, uint32_t *const *out_c,
-                 float *const *out_t, uint32_t flags) {
+                 float *const *out_t, uint32_t flags, bool wait) {
   uint32_t *cp[kChunk];
   float *tp[kChunk];
   for (int32_t i = 0; i < m->n; ++i) {
     HIP_TRY(hipSetDevice(m->dev[i]));
-    if (i > 0) HIP_TRY(hipStreamWaitEvent(m->st[i], m->ev0, 0));
+    if (i > 0 && wait) HIP_TRY(hipStreamWaitEvent(m->st[i], m->ev0, 0));
     for (int32_t f = 0; f < k; ++f) {
       cp[f] = slot_color(m, i, f);
       tp[f] = slot_t(m, i, f);
@@ -208,6 +214,7 @@ int render_chunk(rt_multi *m, const rt_render_params *params, int32_t k, uint32_
     if (int rc = rt_untile_device(m->rc + (size_t)f * m->n * m->cap, m->rt + (size_t)f * m->n * m->cap, m->cap,
                                   out_c[f], out_t[f], m->W, m->H, &all, m->st[0]))
       return rc;
+  HIP_TRY(hipEventRecord(m->rc_free, m->st[0]));
   return RT_OK;
 }
 
@@ -264,6 +271,8 @@ int rt_multi_create(rt_scene *scene, const int32_t *devices, int32_t n, int32_t 
     hipError_t e = hipSetDevice(m->dev[0]);
     if (e == hipSuccess) e = hipEventCreate(&m->ev0);
     if (e == hipSuccess) e = hipEventCreate(&m->ev1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&m->rc_free, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(m->rc_free, m->st[0]);
     if (e != hipSuccess) rc = rterr::set(RT_E_DEVICE, std::string("rt_multi_create: events: ") + hipGetErrorString(e));
   }
   if (rc == RT_OK && m->rccl) {
@@ -347,7 +356,7 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
   }
   uint32_t *oc[1] = {m->fc};
   float *ot[1] = {m->ft};
-  if (int rc = render_chunk(m, p, 1, oc, ot, clear ? RT_FLAG_CLEAR : 0u)) return rc;
+  if (int rc = render_chunk(m, p, 1, oc, ot, clear ? RT_FLAG_CLEAR : 0u, true)) return rc;
   HIP_TRY(hipSetDevice(m->dev[0]));
   HIP_TRY(hipEventRecord(m->ev1, m->st[0]));
   HIP_TRY(hipMemcpyAsync(color, m->fc, (size_t)W * H * 4, hipMemcpyDeviceToHost, m->st[0]));
@@ -372,17 +381,18 @@ int rt_multi_render_device_frames(rt_multi *m, const rt_render_params *params, i
   if (int rc = sync_planes(m)) return rc;
   if (int rc = ensure(m, W, H, frames, false)) return rc;
   hipStream_t cs = (hipStream_t)stream;
+  // the slots start after the caller's queued work
+  HIP_TRY(hipSetDevice(m->dev[0]));
+  HIP_TRY(hipEventRecord(m->ev0, cs));
+  HIP_TRY(hipStreamWaitEvent(m->st[0], m->ev0, 0));
   for (int32_t f0 = 0; f0 < frames; f0 += kChunk) {
     const int32_t k = std::min(kChunk, frames - f0);
-    HIP_TRY(hipSetDevice(m->dev[0]));
-    // the slots start after the caller's queued work (and the previous chunk's untile)
-    HIP_TRY(hipEventRecord(m->ev0, cs));
-    HIP_TRY(hipStreamWaitEvent(m->st[0], m->ev0, 0));
-    if (int rc = render_chunk(m, params + f0, k, d_color + f0, d_t + f0, RT_FLAG_CLEAR)) return rc;
-    HIP_TRY(hipSetDevice(m->dev[0]));
-    HIP_TRY(hipEventRecord(m->ev1, m->st[0]));
-    HIP_TRY(hipStreamWaitEvent(cs, m->ev1, 0));
+    if (int rc = render_chunk(m, params + f0, k, d_color + f0, d_t + f0, RT_FLAG_CLEAR, f0 == 0)) return rc;
   }
+  // the caller's stream waits for the assembled frames
+  HIP_TRY(hipSetDevice(m->dev[0]));
+  HIP_TRY(hipEventRecord(m->ev1, m->st[0]));
+  HIP_TRY(hipStreamWaitEvent(cs, m->ev1, 0));
   return RT_OK;
 }
 
@@ -401,6 +411,7 @@ int rt_multi_destroy(rt_multi *m) {
   HIP_NOTE(hipSetDevice(m->dev[0]));
   if (m->ev0) HIP_NOTE(hipEventDestroy(m->ev0));
   if (m->ev1) HIP_NOTE(hipEventDestroy(m->ev1));
+  if (m->rc_free) HIP_NOTE(hipEventDestroy(m->rc_free));
   delete m;
   return RT_OK;
 }
