@@ -95,6 +95,7 @@ def test_cli_multi_device_reproduces_golden_hash(gpu, name, W, H, mode, devices)
     args = [CLI, data.path(name), "--size", str(W), str(H), "--frames", "2", "--devices", devices]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    out = json.loads(r.stdout)
+    # (RCCL prints its version banner to stdout when the communicator is made)
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["devices"] == len(devices.split(","))
     assert out["hash"] == S.GOLDEN[(name, W, H, mode)]

@@ -290,6 +290,59 @@ def test_drop_in_failure_leaves_no_copy_in_flight(gpu):
     assert np.array_equal(c, rc)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_drop_in_cleared_frames_zero_copy(gpu, pinned):
+    """rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY, the
+    app's frameBuf.clear() + draw) stores the hits straight into HOST memory:
+    into the caller's buffers when rt_host_pin pinned them, else into the
+    scene's pinned staging frame, whose hit box is then copied to the caller
+    and cleared again. A sequence of frames -- cameras with narrow, wide and no
+    hits, a size change, default and primary shading, an injected failure --
+    each equals the same frame through the device-frame path (RT_FLAG_CLEAR
+    alone: every pixel written on the device and downloaded)."""
+    import ctypes as C
+    rt = gpu
+    L = rt.lib()
+    L.rtx_render_inject_failure.argtypes = [C.c_int32]
+    name = "stanford-bunny.obj"
+    sc = S.gpu_scene(name)
+    seq = [(320, 180, "default", (0.0, 0.3, 2.5)), (320, 180, "primary", (0.0, 0.1, 3.5)),
+           (320, 180, "primary", (0.2, 0.1, 0.9)), (320, 180, "default", (0.0, 0.0, -30.0)),
+           (200, 120, "default", (1.2, 0.4, 1.9)), ("fail", None, None, None),
+           (320, 180, "primary", (-0.7, 0.5, 2.2)), (200, 120, "default", (0.4, -0.1, 2.6))]
+    bufs = {}
+    try:
+        for W, H, mode, pos in seq:
+            if W == "fail":
+                L.rtx_render_inject_failure(1)
+                c, t = bufs[(320, 180)]
+                with pytest.raises(rt.RtError, match="injected"):
+                    sc.render(S.params(name, 320, 180, "primary", (0.0, 0.0, 2.5), "gpu"), c, t, cleared=True)
+                continue
+            if (W, H) not in bufs:
+                bufs[(W, H)] = (np.zeros((H, W), np.uint32), np.full((H, W), np.inf, np.float32))
+                if pinned:
+                    for a in bufs[(W, H)]:
+                        rt._lib.check(L.rt_host_pin(a.ctypes.data, a.nbytes))
+            c, t = bufs[(W, H)]
+            c[:] = 0
+            t[:] = np.inf
+            S.set_planes(name, mode, sc)
+            P = S.params(name, W, H, mode, pos, "gpu")
+            sc.render(P, c, t, cleared=True)
+            rc = np.zeros((H, W), np.uint32)
+            rt_ = np.full((H, W), np.inf, np.float32)
+            sc.render(P, rc, rt_, clear=True)
+            assert np.array_equal(c, rc), (W, H, mode, pos, int((c != rc).sum()))
+            assert np.array_equal(t.view(np.uint32), rt_.view(np.uint32)), (W, H, mode, pos)
+    finally:
+        L.rtx_render_inject_failure(0)
+        if pinned:
+            for c, t in bufs.values():
+                L.rt_host_unpin(c.ctypes.data)
+                L.rt_host_unpin(t.ctypes.data)
+
+
 def test_hits_only_needs_clear(gpu):
     from rtamd import _lib
     sc = S.gpu_scene("cube.obj")

@@ -326,9 +326,14 @@ __device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
 #ifndef RT_PEER_RELEASE
 #define RT_PEER_RELEASE 1
 #endif
+// Internal frame flag (never a caller's): the frame is HOST memory mapped to
+// the device (rt_render's zero-copy download of a cleared frame), written
+// with the same system-scope stores and release as a peer's frame.
+constexpr uint32_t kFlagHostFrame = 1u << 16;
+constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL | kFlagHostFrame;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
-  if (flags & RT_FLAG_TILE_NATURAL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 #endif
 }
 
@@ -390,7 +395,7 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     const f3 d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
     // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
     // full frame's own row (a peer's frame mapped over xGMI)
-    const bool peer = (fa.flags & RT_FLAG_TILE_NATURAL) != 0;
+    const bool peer = (fa.flags & kSysStoreFlags) != 0;
     const int yb = peer ? yo : yl;
     // 32-bit pixel index (check_params caps W*H at 2^31): one register live
     // across the traversal instead of two
@@ -886,7 +891,7 @@ void render_pump_kernel(P sc, FrameBatch fb, PersistQ q, int32_t nframes, int32_
   const int lane = threadIdx.x & 63;
   const uint32_t xcc = __builtin_amdgcn_s_getreg(0x1814) & 7;  // HW_REG_XCC_ID
   const bool clear = (F.flags & RT_FLAG_CLEAR) != 0, hits_only = (F.flags & RT_FLAG_HITS_ONLY) != 0;
-  const bool peer = (F.flags & RT_FLAG_TILE_NATURAL) != 0;
+  const bool peer = (F.flags & kSysStoreFlags) != 0;
   const uint32_t isz = 64u * q.gx * q.gy;  // pixels per item
   ItemStream is{xcc, q_claim(q.heads + xcc * q.stride)};
   uint32_t cur = take_item(q, is, xcc, lane), off = 0;
@@ -1139,6 +1144,13 @@ struct rt_scene {
   hipEvent_t xev = nullptr;
   int32_t *d_hit_box = nullptr;  // rt_render: FrameArgs::hit_box of its frame (4 words)
   int32_t *h_hit_box = nullptr;  // pinned host copy of it
+  // rt_render's staging frame for a cleared frame on pageable buffers: pinned
+  // host memory the kernel stores its hits into (zero-copy), kept cleared
+  uint32_t *stage_c = nullptr;
+  float *stage_t = nullptr;
+  size_t stage_cap = 0;
+  int32_t stage_W = 0, stage_H = 0;
+  bool stage_dirty = true;
   // cost-ordered block schedule (see launch_render): per-block cost of the
   // last frame rendered with sched_grid blocks, and the block order derived
   // from it; sched_on = false renders in plain blockIdx order
@@ -2053,6 +2065,8 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->xev) HIP_NOTE(hipEventDestroy(s->xev));
   if (s->d_hit_box) HIP_NOTE(hipFree(s->d_hit_box));
   if (s->h_hit_box) HIP_NOTE(hipHostFree(s->h_hit_box));
+  if (s->stage_c) HIP_NOTE(hipHostFree(s->stage_c));
+  if (s->stage_t) HIP_NOTE(hipHostFree(s->stage_t));
   for (hipStream_t x : s->xs)
     if (x) HIP_NOTE(hipStreamDestroy(x));
   HIP_NOTE(hipSetDevice(prev));
@@ -2178,6 +2192,118 @@ int rt_ipc_close(void *d_ptr) {
 std::atomic<int> g_render_fault{0};
 std::atomic<int64_t> g_render_drains{0};
 
+namespace {
+
+// Host ranges pinned through rt_host_pin (base -> bytes): rt_render writes a
+// cleared frame's hits straight into such buffers.
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pins;
+
+// The device address of host range [p, p + bytes) when it lies inside one
+// range pinned by rt_host_pin, else nullptr.
+void *pinned_device_ptr(const void *p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  uintptr_t base = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.upper_bound(a);
+    if (it == g_pins.begin()) return nullptr;
+    --it;
+    if (a < it->first || a + bytes > it->first + it->second) return nullptr;
+    base = it->first;
+  }
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, (void *)base, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();  // (not mapped: take the staged path)
+    return nullptr;
+  }
+  return (char *)d + (a - base);
+}
+
+// RTAMD_DROPIN_ZC=0: rt_render's cleared frames take the device frame + boxed
+// download instead of the zero-copy path (A/B switch)
+bool dropin_zero_copy() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_DROPIN_ZC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY: the app's
+// frameBuf.clear() + draw, src/main.cpp:197,203): only hit pixels differ from
+// the caller's buffers (raytracing.cpp:91-94), and the kernel stores exactly
+// those -- with system-scope stores into HOST memory, so no download follows
+// the kernel:
+//  * buffers pinned by rt_host_pin: the hits go straight into them;
+//  * pageable buffers: into the scene's pinned staging frame, which is kept
+//    cleared; after the kernel the host copies the hits' bounding box to the
+//    caller's buffers and clears it in the staging frame again (OpenMP rows).
+int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *t, int32_t W, int32_t H,
+                             float *ms) {
+  const size_t px = (size_t)W * H;
+  hipStream_t a = s->xs[0];
+  struct Drain {
+    hipStream_t a;
+    ~Drain() {
+      if (hipStreamSynchronize(a) == hipSuccess) g_render_drains.fetch_add(1);
+    }
+  } drain{a};
+  void *dc = pinned_device_ptr(color, px * 4), *dt = pinned_device_ptr(t, px * 4);
+  const bool direct = dc && dt;
+  fa.flags |= RT_FLAG_HITS_ONLY | kFlagHostFrame;
+  fa.hit_box = nullptr;
+  if (direct) {
+    fa.color = (uint32_t *)dc;
+    fa.t = (float *)dt;
+  } else {
+    if (px > s->stage_cap) {
+      if (s->stage_c) HIP_NOTE(hipHostFree(s->stage_c));
+      if (s->stage_t) HIP_NOTE(hipHostFree(s->stage_t));
+      s->stage_c = nullptr;
+      s->stage_t = nullptr;
+      s->stage_cap = 0;
+      HIP_TRY(hipHostMalloc(&s->stage_c, px * 4, hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc(&s->stage_t, px * 4, hipHostMallocDefault));
+      s->stage_cap = px;
+      s->stage_dirty = true;
+    }
+    if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
+      rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
+      s->stage_W = W;
+      s->stage_H = H;
+      s->stage_dirty = false;
+    }
+    void *sc = nullptr, *st = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
+    HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
+    fa.color = (uint32_t *)sc;
+    fa.t = (float *)st;
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_hit_box, 0x7FFFFFFF, 4, a));
+    fa.hit_box = s->d_hit_box;
+  }
+  if (g_render_fault.load() > 0) {
+    g_render_fault.fetch_sub(1);
+    return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
+  }
+  HIP_TRY(hipEventRecord(s->ev0, a));
+  if (!direct) s->stage_dirty = true;  // until its box is cleared again below
+  if (int rc = launch_render(s, fa, a)) return rc;
+  HIP_TRY(hipEventRecord(s->ev1, a));
+  if (!direct) HIP_TRY(hipMemcpyAsync(s->h_hit_box, s->d_hit_box, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, a));
+  HIP_TRY(hipStreamSynchronize(a));
+  if (!direct) {
+    const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
+    if (x0 <= x1 && y0 <= y1)
+      rth::copy_rect_clear(color, t, s->stage_c, s->stage_t, W, x0, x1, y0, y1, y1 - y0 >= 64 ? 8 : 1);
+    s->stage_dirty = false;
+  }
+  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  return RT_OK;
+}
+
+}  // namespace
+
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
               uint32_t flags, float *ms) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
@@ -2189,6 +2315,10 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   FrameArgs fa;
   if ((rc = fill_frame(fa, p, nullptr, nullptr, W, H, flags & ~RT_FLAG_HITS_ONLY, nullptr))) return rc;
   const size_t px = (size_t)W * H;
+  if (flags == (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) && dropin_zero_copy()) {
+    if ((rc = ensure_events(s)) || (rc = ensure_copy_streams(s))) return rc;
+    return render_cleared_zero_copy(s, fa, color, t, W, H, ms);
+  }
   if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s)) || (rc = ensure_copy_streams(s))) return rc;
   fa.color = s->d_color;
   fa.t = s->d_t;
@@ -2272,12 +2402,18 @@ int64_t rtx_render_drain_count(void) { return g_render_drains.load(); }
 
 int rt_host_pin(void *ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad host range");
-  HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+  HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped));
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pins[(uintptr_t)ptr] = (size_t)bytes;
   return RT_OK;
 }
 
 int rt_host_unpin(void *ptr) {
   if (!ptr) return set_err(RT_E_INVALID, "NULL pointer");
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pins.erase((uintptr_t)ptr);
+  }
   HIP_TRY(hipHostUnregister(ptr));
   return RT_OK;
 }
