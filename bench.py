@@ -566,6 +566,8 @@ def drop_in(scene, params, W, H, frames=16):
                     wall += time.perf_counter() - t0
                 out[f"{'pinned' if pinned else 'pageable'}_{how}_ms"] = round(wall * 1e3 / frames, 4)
                 out.setdefault("kernel_ms", round(statistics.median(ks), 4))
+                if how == "cleared":  # the zero-copy kernel stores into host memory: its own time
+                    out[f"{'pinned' if pinned else 'pageable'}_cleared_kernel_ms"] = round(statistics.median(ks), 4)
         finally:
             if pinned:
                 L.rt_host_unpin(c.ctypes.data)

@@ -326,11 +326,12 @@ __device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
 #ifndef RT_PEER_RELEASE
 #define RT_PEER_RELEASE 1
 #endif
-// Internal frame flag (never a caller's): the frame is HOST memory mapped to
-// the device (rt_render's zero-copy download of a cleared frame), written
-// with the same system-scope stores and release as a peer's frame.
-constexpr uint32_t kFlagHostFrame = 1u << 16;
-constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL | kFlagHostFrame;
+// (A frame in HOST memory -- rt_render's zero-copy cleared frames -- takes the
+// device frame's stores: the dispatch's end-of-kernel system-scope release,
+// before rt_render's stream synchronisation, makes them visible to the host.
+// A per-wave system-scope fence there costs an L2 write-back per wave: the
+// one-frame kernel's 32 k waves took the frame from 0.19 to ~0.38 ms.)
+constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
   if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -2233,7 +2234,7 @@ bool dropin_zero_copy() {
 // rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY: the app's
 // frameBuf.clear() + draw, src/main.cpp:197,203): only hit pixels differ from
 // the caller's buffers (raytracing.cpp:91-94), and the kernel stores exactly
-// those -- with system-scope stores into HOST memory, so no download follows
+// those -- into HOST memory (zero-copy), so no download follows
 // the kernel:
 //  * buffers pinned by rt_host_pin: the hits go straight into them;
 //  * pageable buffers: into the scene's pinned staging frame, which is kept
@@ -2251,7 +2252,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   } drain{a};
   void *dc = pinned_device_ptr(color, px * 4), *dt = pinned_device_ptr(t, px * 4);
   const bool direct = dc && dt;
-  fa.flags |= RT_FLAG_HITS_ONLY | kFlagHostFrame;
+  fa.flags |= RT_FLAG_HITS_ONLY;
   fa.hit_box = nullptr;
   if (direct) {
     fa.color = (uint32_t *)dc;

@@ -1115,18 +1115,24 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
     return clamp_med3(q.x, bmin.x, bmax.x) == q.x && clamp_med3(q.y, bmin.y, bmax.y) == q.y &&
            clamp_med3(q.z, bmin.z, bmax.z) == q.z;
   };
-  while (inside(p)) {
-    const float s = oct_sdf(c, bmin, inv_s, p);
+  // The march's state (t, p, s) is all the loop carries; the hit is read off
+  // it after the loop, so no output is a loop-carried value (the outputs
+  // written inside the loop made the compiler copy ~13 registers per step).
+  float s = 0.0f;
+  bool in = inside(p);
+  while (in) {
+    s = oct_sdf(c, bmin, inv_s, p);
     cnt.add(C_OCT_STEP, 1);
-    if (s < 1e-4f) {
-      out_t = t + s;
-      out_p = p;
-      return true;
-    }
+    if (s < 1e-4f) break;  // hit: `in` stays true
     t += s;
     p = o + t * d;
+    in = inside(p);
   }
-  return false;
+  if (in) {
+    out_t = t + s;
+    out_p = p;
+  }
+  return in;
 }
 
 // Where a leaf march hit: the leaf (node index, integer box coordinates at
@@ -1222,8 +1228,13 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
     cswap(s0, b0, s1, b1);
     cswap(s1, b1, s2, b2);
     cswap(s0, b0, s1, b1);
-    const float k0 = P, k1 = __builtin_fmaxf(P, s0), k2 = __builtin_fmaxf(P, s1), k3 = __builtin_fmaxf(P, s2);
-    const float m0 = __builtin_fminf(Q, s0), m1 = __builtin_fminf(Q, s1), m2 = __builtin_fminf(Q, s2), m3 = Q;
+    // max / min of finite values as one v_med3 against -/+inf: the same value,
+    // and unlike fmaxf / fminf the compiler adds no operand canonicalisation
+    // (the s values come out of selects it cannot prove canonical)
+    auto mx2 = [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); };
+    auto mn2 = [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); };
+    const float k0 = P, k1 = mx2(P, s0), k2 = mx2(P, s1), k3 = mx2(P, s2);
+    const float m0 = mn2(Q, s0), m1 = mn2(Q, s1), m2 = mn2(Q, s2), m3 = Q;
     const bool e0 = !(m0 < 0.0f || k0 > m0) && k0 > 0.0f, e1 = !(m1 < 0.0f || k1 > m1) && k1 > 0.0f;
     const bool e2 = !(m2 < 0.0f || k2 > m2) && k2 > 0.0f, e3 = !(m3 < 0.0f || k3 > m3) && k3 > 0.0f;
     exact = !(s0 < s1 && s1 < s2) || (e0 && e1 && !(k0 < k1)) || (e1 && e2 && !(k1 < k2)) ||
@@ -1348,11 +1359,15 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   if (root == 0 || root == rtl::kOctNeverHits) {
     cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return RAY_MISS;
+    float lt;
+    f3 lp;
+    if (!oct_leaf<FAST>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar, lt,
+                        lp, cnt))
+      return RAY_MISS;
+    out_t = lt;
+    hp.p = lp;
     hp.node = 0; hp.ix = 0; hp.iy = 0; hp.iz = 0; hp.depth = 0;
-    return oct_leaf<FAST>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar,
-                          out_t, hp.p, cnt)
-               ? RAY_HIT
-               : RAY_MISS;
+    return RAY_HIT;
   }
   f3 bmin, bmax;
   float inv_s;
@@ -1413,7 +1428,11 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     oct_box(cxyz.ix(), cxyz.iy(), cxyz.iz(), depth + 1, bmin, bmax, inv_s);
     if (leaf) {
       cnt.add(C_OCT_LEAF, 1);
-      if (oct_leaf<FAST>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, out_t, hp.p, cnt)) {
+      float lt;
+      f3 lp;
+      if (oct_leaf<FAST>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, lt, lp, cnt)) {
+        out_t = lt;
+        hp.p = lp;
         hp.node = cn; hp.ix = cxyz.ix(); hp.iy = cxyz.iy(); hp.iz = cxyz.iz(); hp.depth = depth + 1;
         return RAY_HIT;
       }
