@@ -118,6 +118,22 @@ __device__ __forceinline__ void bbox_isect(f3 bmin, f3 bmax, f3 o, f3 inv, float
     bbox_intersection(bmin, bmax, o, inv, tmin, tmax, t1, t2);
 }
 
+// max / min of two non-NaN floats as the bare instruction. fmaxf / fminf
+// lower to the same v_max_f32 / v_min_f32 but, in the kernels' IEEE mode, with
+// a canonicalising v_max_f32 x, x in front of every operand the compiler cannot
+// prove canonical (results of selects, kernel arguments); for non-NaN operands
+// the value is the same.
+__device__ __forceinline__ float vmax_f32(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmin_f32(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // std::min(std::max(x, lo), hi) for a finite (non-NaN) x and lo < hi, as one
 // v_med3_f32 (the two forms differ only in the sign of a zero result, which
 // callers never feed into arithmetic)

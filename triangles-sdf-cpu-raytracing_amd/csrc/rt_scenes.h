@@ -1206,8 +1206,11 @@ template <bool FAST>
 __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar,
                                            uint32_t keep, uint32_t &list, uint32_t &cnt) {
   const f3 center{(bmin.x + bmax.x) / 2.0f, (bmin.y + bmax.y) / 2.0f, (bmin.z + bmax.z) / 2.0f};
-  const f3 diff = center - bmin;
-  const f3 hi{center.x + diff.x, center.y + diff.y, center.z + diff.z};  // == bmax, the child max
+  // divide_box_8's upper child max, center + (center - boxMin), IS bmax: every
+  // value on the chain is an exact dyadic (oct_box), so the add is exact; the
+  // slab distances below use bmax directly (the same operands, the same
+  // bits), which the child visit's leaf test computes too
+  const f3 hi = bmax;
   const float x0 = (bmin.x - o.x) * inv.x, x1 = (center.x - o.x) * inv.x, x2 = (hi.x - o.x) * inv.x;
   const float y0 = (bmin.y - o.y) * inv.y, y1 = (center.y - o.y) * inv.y, y2 = (hi.y - o.y) * inv.y;
   const float z0 = (bmin.z - o.z) * inv.z, z1 = (center.z - o.z) * inv.z, z2 = (hi.z - o.z) * inv.z;
@@ -1228,17 +1231,23 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
     cswap(s0, b0, s1, b1);
     cswap(s1, b1, s2, b2);
     cswap(s0, b0, s1, b1);
-    // max / min of finite values as one v_med3 against -/+inf: the same value,
-    // and unlike fmaxf / fminf the compiler adds no operand canonicalisation
-    // (the s values come out of selects it cannot prove canonical)
-    auto mx2 = [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); };
-    auto mn2 = [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); };
-    const float k0 = P, k1 = mx2(P, s0), k2 = mx2(P, s1), k3 = mx2(P, s2);
-    const float m0 = mn2(Q, s0), m1 = mn2(Q, s1), m2 = mn2(Q, s2), m3 = Q;
-    const bool e0 = !(m0 < 0.0f || k0 > m0) && k0 > 0.0f, e1 = !(m1 < 0.0f || k1 > m1) && k1 > 0.0f;
-    const bool e2 = !(m2 < 0.0f || k2 > m2) && k2 > 0.0f, e3 = !(m3 < 0.0f || k3 > m3) && k3 > 0.0f;
-    exact = !(s0 < s1 && s1 < s2) || (e0 && e1 && !(k0 < k1)) || (e1 && e2 && !(k1 < k2)) ||
-            (e2 && e3 && !(k2 < k3));
+    // max / min of these finite values as the bare v_max_f32 / v_min_f32: the
+    // same value, without the operand canonicalisation the compiler puts in
+    // front of fmaxf / fminf (it cannot prove the selects' results canonical)
+    const float k0 = P, k1 = vmax_f32(P, s0), k2 = vmax_f32(P, s1), k3 = vmax_f32(P, s2);
+    const float m0 = vmin_f32(Q, s0), m1 = vmin_f32(Q, s1), m2 = vmin_f32(Q, s2), m3 = Q;
+    // entered and kept: the reference's !(tMax < 0 || tMin > tMax) && t > 0;
+    // with no NaN, k > 0 and k <= m imply m >= 0, so two compares suffice
+    // (written so the compiler does not fold them into an fmax that needs
+    // canonicalised operands)
+    const bool e0 = (k0 > 0.0f) & (m0 >= k0), e1 = (k1 > 0.0f) & (m1 >= k1);
+    const bool e2 = (k2 > 0.0f) & (m2 >= k2), e3 = (k3 > 0.0f) & (m3 >= k3);
+    // Ties among the kept entries: with s0 < s1 < s2, k_i = max(P, s_{i-1}) is
+    // non-decreasing and k_i == k_{i+1} only when both are P, i.e. s_i <= P;
+    // entry i also needs m_i = min(Q, s_i) >= k_i = P, so a tie of two kept
+    // entries implies s_i == P. Testing s_i == P directly is therefore a
+    // superset of the tie test (a spare exact expansion is still exact).
+    exact = !(s0 < s1 && s1 < s2) || s0 == P || s1 == P || s2 == P;
     const uint32_t c0 = (px ? 0u : 4u) | (py ? 0u : 2u) | (pz ? 0u : 1u);
     const uint32_t c1 = c0 ^ b0, c2 = c1 ^ b1, c3 = c2 ^ b2;
     // pack from the back so the first visit ends in the low bits
