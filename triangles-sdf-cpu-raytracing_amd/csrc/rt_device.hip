@@ -1033,6 +1033,17 @@ __global__ void clear_kernel(uint32_t *c, float *t, int64_t n) {
   }
 }
 
+// FrameBuffer::clear() of the rectangle [x0, x1] x [y0, y1] of a W-wide frame
+// (rt_render's staging frame, after its hit box was copied out): one thread
+// per pixel, blockIdx.y = row.
+__global__ void clear_rect_kernel(uint32_t *c, float *t, int32_t W, int32_t x0, int32_t x1, int32_t y0) {
+  const int32_t x = x0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (x > x1) return;
+  const size_t i = (size_t)(y0 + (int32_t)blockIdx.y) * (size_t)W + (size_t)x;
+  c[i] = 0u;
+  t[i] = kInf;
+}
+
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
                               float *t, int W, int H, int band_rows, int nranks) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2244,10 +2255,14 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
                              float *ms) {
   const size_t px = (size_t)W * H;
   hipStream_t a = s->xs[0];
+  // every return waits for stream a while it may still touch the caller's
+  // buffers; the staging frame's re-clear (below) is the library's own and
+  // is left running when the call returns
   struct Drain {
     hipStream_t a;
+    bool on = true;
     ~Drain() {
-      if (hipStreamSynchronize(a) == hipSuccess) g_render_drains.fetch_add(1);
+      if (on && hipStreamSynchronize(a) == hipSuccess) g_render_drains.fetch_add(1);
     }
   } drain{a};
   void *dc = pinned_device_ptr(color, px * 4), *dt = pinned_device_ptr(t, px * 4);
@@ -2259,13 +2274,18 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     fa.t = (float *)dt;
   } else {
     if (px > s->stage_cap) {
+      HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
       if (s->stage_c) HIP_NOTE(hipHostFree(s->stage_c));
       if (s->stage_t) HIP_NOTE(hipHostFree(s->stage_t));
       s->stage_c = nullptr;
       s->stage_t = nullptr;
       s->stage_cap = 0;
-      HIP_TRY(hipHostMalloc(&s->stage_c, px * 4, hipHostMallocDefault));
-      HIP_TRY(hipHostMalloc(&s->stage_t, px * 4, hipHostMallocDefault));
+      // non-coherent: the GPU may cache the kernel's stores in its L2 until the
+      // kernel's end-of-dispatch release (coherent host memory took the kernel
+      // from 0.195 to 0.280 ms at 1080p); the host reads only after the stream
+      // synchronisation, and the CPU side stays coherent (snooped PCIe writes)
+      HIP_TRY(hipHostMalloc(&s->stage_c, px * 4, hipHostMallocNonCoherent));
+      HIP_TRY(hipHostMalloc(&s->stage_t, px * 4, hipHostMallocNonCoherent));
       s->stage_cap = px;
       s->stage_dirty = true;
     }
@@ -2293,13 +2313,25 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   HIP_TRY(hipEventRecord(s->ev1, a));
   if (!direct) HIP_TRY(hipMemcpyAsync(s->h_hit_box, s->d_hit_box, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, a));
   HIP_TRY(hipStreamSynchronize(a));
+  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   if (!direct) {
     const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
-    if (x0 <= x1 && y0 <= y1)
-      rth::copy_rect_clear(color, t, s->stage_c, s->stage_t, W, x0, x1, y0, y1, y1 - y0 >= 64 ? 8 : 1);
+    if (x0 <= x1 && y0 <= y1) {
+      // the hits' box to the caller (host threads), then the same box of the
+      // staging frame cleared again by the GPU, in stream order before the
+      // next frame's kernel; the call does not wait for it
+      rth::copy_rect(color, t, s->stage_c, s->stage_t, W, x0, x1, y0, y1, y1 - y0 >= 32 ? 8 : 1);
+      drain.on = false;
+      void *sc = nullptr, *st = nullptr;
+      HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
+      HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
+      const int32_t w = x1 - x0 + 1;
+      clear_rect_kernel<<<dim3((unsigned)((w + 255) / 256), (unsigned)(y1 - y0 + 1)), 256, 0, a>>>(
+          (uint32_t *)sc, (float *)st, W, x0, x1, y0);
+      HIP_TRY(hipGetLastError());
+    }
     s->stage_dirty = false;
   }
-  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   return RT_OK;
 }
 

@@ -1008,17 +1008,14 @@ void camera_matrices(const float pos[3], const float target[3], const float up[3
   invert(pr, proj_inv);
 }
 
-void copy_rect_clear(uint32_t *dc, float *dt, uint32_t *sc, float *st, int64_t W, int32_t x0, int32_t x1,
-                     int32_t y0, int32_t y1, int threads) {
+void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t x0, int32_t x1,
+               int32_t y0, int32_t y1, int threads) {
   const size_t w = (size_t)(x1 - x0 + 1);
-  const float inf = std::numeric_limits<float>::infinity();
 #pragma omp parallel for schedule(static) num_threads(threads) if (threads > 1)
   for (int32_t y = y0; y <= y1; ++y) {
     const size_t o = (size_t)y * (size_t)W + (size_t)x0;
     std::memcpy(dc + o, sc + o, w * 4);
     std::memcpy(dt + o, st + o, w * 4);
-    std::memset(sc + o, 0, w * 4);
-    std::fill(st + o, st + o + w, inf);
   }
 }
 

@@ -1050,15 +1050,25 @@ __device__ __forceinline__ void oct_local(f3 bmin, float inv_s, f3 p, f3 &a, f3 
 __device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, float inv_s, f3 p) {
   f3 a, b;
   oct_local(bmin, inv_s, p, a, b);
-  float res = 0.0f;  // octree_raytracing.cpp:36-55, values[(x<<2)+(y<<1)+z]
-  res += c.v[0] * b.x * b.y * b.z;
-  res += c.v[1] * b.x * b.y * a.z;
-  res += c.v[2] * b.x * a.y * b.z;
-  res += c.v[3] * b.x * a.y * a.z;
-  res += c.v[4] * a.x * b.y * b.z;
-  res += c.v[5] * a.x * b.y * a.z;
-  res += c.v[6] * a.x * a.y * b.z;
-  res += c.v[7] * a.x * a.y * a.z;
+  // octree_raytracing.cpp:36-55, values[(x<<2)+(y<<1)+z]: each term is
+  // ((v * X) * Y) * Z, the reference's product order; the two terms that
+  // differ only in Z (b.z / a.z) go through the packed-math unit together
+  // (v2f: the same IEEE multiplies per element), and the sum keeps the
+  // reference's order
+  const v2f zz{b.z, a.z};
+  const v2f t01 = v2f{c.v[0], c.v[1]} * b.x * b.y * zz;
+  const v2f t23 = v2f{c.v[2], c.v[3]} * b.x * a.y * zz;
+  const v2f t45 = v2f{c.v[4], c.v[5]} * a.x * b.y * zz;
+  const v2f t67 = v2f{c.v[6], c.v[7]} * a.x * a.y * zz;
+  float res = 0.0f;
+  res += t01.x;
+  res += t01.y;
+  res += t23.x;
+  res += t23.y;
+  res += t45.x;
+  res += t45.y;
+  res += t67.x;
+  res += t67.y;
   return res;
 }
 
