@@ -1480,7 +1480,15 @@ int resident_blocks(K kernel, int &blocks, int &dev_cached, int block = kBlock) 
     int per_cu = 0, cus = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    blocks = std::max(1, per_cu) * std::max(1, cus);
+    // RTAMD_PERSIST_OVERSUB=k launches k x the resident workgroups (A/B
+    // switch: extra waves start as resident ones leave and exit at once when
+    // the queue is drained)
+    static const int oversub = [] {
+      const char *e = std::getenv("RTAMD_PERSIST_OVERSUB");
+      const int v = e ? std::atoi(e) : 1;
+      return v >= 1 && v <= 8 ? v : 1;
+    }();
+    blocks = std::max(1, per_cu) * std::max(1, cus) * oversub;
     dev_cached = dev;
   }
   return RT_OK;
