@@ -323,6 +323,46 @@ def test_sixteen_frames_per_launch(gpu):
         assert np.array_equal(pt[k].cpu().numpy().view(np.uint32), single[k][1][rows].reshape(-1)), k
 
 
+@pytest.mark.parametrize("mode", ["primary", "default"])
+def test_band_order_is_output_neutral(gpu, mode):
+    """The heavy-first tile order of row-band launches (band_sched: each
+    stream's previous band launch's tile costs order its next one) changes
+    only the dispatch order: consecutive multi-frame band launches on one
+    stream (the first unordered, the next ones ordered) equal the same bands
+    rendered one frame at a time, bit for bit; a change of band geometry on
+    the stream drops the order and still renders right."""
+    import ctypes as C
+
+    import rtamd
+    from rtamd._lib import lib
+    torch = pytest.importorskip("torch")
+    from rtamd.workloads import orbit_positions
+    L = lib()
+    name = "stanford-bunny.obj"
+    s = S.gpu_scene(name)
+    S.set_planes(name, mode, s)
+    st = torch.cuda.Stream()
+    orbit = orbit_positions(64)
+    for W, H, tile, launches in ((320, 240, rtamd.Tile(8, 1, 4, 0), 4), (256, 200, rtamd.Tile(8, 0, 3, 0), 2),
+                                 (320, 240, rtamd.Tile(8, 1, 4, 0), 2)):
+        npx = L.rt_tile_pixels(W, H, C.byref(tile))
+        for j in range(launches):
+            P = [S.params(name, W, H, mode, orbit[(7 * j + 3 * i) % 64], module="gpu") for i in range(3)]
+            pc = [torch.zeros(npx, dtype=torch.int32, device="cuda") for _ in P]
+            pt = [torch.zeros(npx, dtype=torch.float32, device="cuda") for _ in P]
+            with torch.cuda.stream(st):
+                s.render_device_frames(P, [c.data_ptr() for c in pc], [t.data_ptr() for t in pt], W, H,
+                                       rtamd.RT_FLAG_CLEAR, tile=tile, stream=st.cuda_stream)
+            st.synchronize()
+            for k, prm in enumerate(P):
+                c1 = torch.zeros(npx, dtype=torch.int32, device="cuda")
+                t1 = torch.zeros(npx, dtype=torch.float32, device="cuda")
+                s.render_device(prm, c1.data_ptr(), t1.data_ptr(), W, H, clear=True, tile=tile)
+                torch.cuda.synchronize()
+                assert torch.equal(pc[k], c1), (W, H, j, k)
+                assert torch.equal(pt[k].view(torch.int32), t1.view(torch.int32)), (W, H, j, k)
+
+
 SORT8_PAIRS = [(0, 1), (2, 3), (4, 5), (6, 7), (0, 2), (1, 3), (4, 6), (5, 7), (1, 2), (5, 6),
                (0, 4), (3, 7), (1, 5), (2, 6), (1, 4), (3, 6), (2, 4), (3, 5), (3, 4)]
 

@@ -602,12 +602,20 @@ void render_batch_kernel(S sc, PlaneDev pl, FrameBatch fb) {
     const int lane = threadIdx.x & 63;
 #if RT_BATCH_INTERLEAVE
     const uint32_t n = gridDim.z, b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    const uint32_t f = b % n, tl = b / n, tx = tl % gridDim.x, ty = tl / gridDim.x;
+    // heavy-first tile order of row bands (fb.f[0].order, from the previous
+    // launch's recorded tile costs on this stream; band_sched)
+    const uint32_t f = b % n, tl = fb.f[0].order ? fb.f[0].order[b / n] : b / n;
+    const uint32_t tx = tl % gridDim.x, ty = tl / gridDim.x;
 #else
-    const uint32_t f = blockIdx.z, tx = blockIdx.x, ty = blockIdx.y;
+    const uint32_t f = blockIdx.z, tl = blockIdx.y * gridDim.x + blockIdx.x, tx = blockIdx.x, ty = blockIdx.y;
 #endif
+    const uint64_t c0 = fb.f[0].cost ? __builtin_amdgcn_s_memtime() : 0;
     render_pixels<S, SLOTS, GENERAL, 0, kBBlock>(sc, pl, fb.f[f], cnt, stk, (int)tx * 8 + (lane & 7),
                                                  (int)ty * 8 + (lane >> 3));
+    if (fb.f[0].cost && lane == 0) {  // this tile's cost: the slowest of its frames' waves
+      const uint64_t dc = __builtin_amdgcn_s_memtime() - c0;
+      atomicMax(fb.f[0].cost + tl, (uint32_t)(dc < 0xFFFFFFFFull ? dc : 0xFFFFFFFFull));
+    }
   }
   peer_release(fb.f[0].flags);
 }
@@ -1422,6 +1430,52 @@ int stream_queue(hipStream_t stream, uint32_t **out) {
   return RT_OK;
 }
 
+// Heavy-first order of the block dispatch for row bands (a rank's 1/N of each
+// frame at N > 1): with so little work per launch, a rank's time is its
+// slowest tiles' chains (silhouette tiles) unless they start first. Each
+// (device, stream) keeps the per-tile cost of its previous band launch (the
+// slowest wave of each tile, any frame) and the order derived from it
+// (order_kernel: half-octave cost classes, heaviest first); consecutive orbit
+// frames keep their heavy tiles near the model's outline, so the last launch
+// predicts the next. Output-neutral: only the dispatch order changes.
+// RTAMD_BAND_ORDER=0 switches it off (A/B).
+struct BandSched {
+  uint32_t *cost = nullptr, *order = nullptr;
+  uint32_t ntiles = 0;
+  bool valid = false;
+};
+std::map<std::pair<int, hipStream_t>, BandSched> g_band_sched;  // (under g_queue_mu)
+
+bool band_order_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_BAND_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int band_sched(hipStream_t stream, uint32_t ntiles, BandSched **out) {
+  *out = nullptr;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_queue_mu);
+  BandSched &b = g_band_sched[{dev, stream}];
+  if (b.ntiles != ntiles) {  // new band geometry: fresh buffers in stream order, no order yet
+    if (b.cost) HIP_NOTE(hipFreeAsync(b.cost, stream));
+    if (b.order) HIP_NOTE(hipFreeAsync(b.order, stream));
+    b = BandSched{};
+    void *c = nullptr, *o = nullptr;
+    HIP_TRY(hipMallocAsync(&c, (size_t)ntiles * 4, stream));
+    HIP_TRY(hipMallocAsync(&o, (size_t)ntiles * 4, stream));
+    HIP_TRY(hipMemsetAsync(c, 0, (size_t)ntiles * 4, stream));
+    b.cost = (uint32_t *)c;
+    b.order = (uint32_t *)o;
+    b.ntiles = ntiles;
+  }
+  *out = &b;
+  return RT_OK;
+}
+
 // diagnostic per-wave stamps of the persistent launches (rtx_set_persist_stamps)
 unsigned long long *g_persist_stamps = nullptr;
 int64_t g_persist_stamps_cap = 0;
@@ -1609,10 +1663,30 @@ int launch_batch_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBatc
                    : launch_persist_t<S, MAXD, false>(s, sc, pl, fb, n, group, stream);
   }
   const dim3 grid((fb.f[0].W + kBTile - 1) / kBTile, (fb.f[0].rows_local + kBTile - 1) / kBTile, n);
+  BandSched *bs = nullptr;
+  if (kBBlock == 64 && RT_BATCH_INTERLEAVE && fb.f[0].nranks > 1 && band_order_enabled()) {
+    if (const int rc = band_sched(stream, grid.x * grid.y, &bs)) return rc;
+  }
+  const FrameBatch *fbp = &fb;
+  FrameBatch fbo;
+  if (bs) {
+    fbo = fb;
+    fbo.f[0].order = bs->valid ? bs->order : nullptr;
+    fbo.f[0].cost = bs->cost;
+    fbp = &fbo;
+  }
   if (general)
-    render_batch_kernel<S, MAXD, true><<<grid, kBBlock, 0, stream>>>(sc, pl, fb);
+    render_batch_kernel<S, MAXD, true><<<grid, kBBlock, 0, stream>>>(sc, pl, *fbp);
   else
-    render_batch_kernel<S, MAXD, false><<<grid, kBBlock, 0, stream>>>(sc, pl, fb);
+    render_batch_kernel<S, MAXD, false><<<grid, kBBlock, 0, stream>>>(sc, pl, *fbp);
+  if (bs) {  // this launch's tile costs -> the next launch's order (and the costs cleared)
+    // one wave: it takes the first wave slot the other stream's launch frees
+    // (a 1024-thread block would wait for a whole CU and hold this stream's
+    // next launch behind it)
+    order_kernel<<<1, 64, 0, stream>>>(bs->cost, bs->order, bs->ntiles);
+    HIP_TRY(hipGetLastError());
+    bs->valid = true;
+  }
   return RT_OK;
 }
 
@@ -2160,6 +2234,12 @@ int rt_stream_release(void *stream) {
   uint32_t *p = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_queue_mu);
+    auto b = g_band_sched.find({dev, (hipStream_t)stream});
+    if (b != g_band_sched.end()) {  // the band order state (band_sched), freed in stream order too
+      if (b->second.cost) HIP_NOTE(hipFreeAsync(b->second.cost, (hipStream_t)stream));
+      if (b->second.order) HIP_NOTE(hipFreeAsync(b->second.order, (hipStream_t)stream));
+      g_band_sched.erase(b);
+    }
     auto it = g_queues.find({dev, (hipStream_t)stream});
     if (it == g_queues.end()) return RT_OK;
     p = it->second;
