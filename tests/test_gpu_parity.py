@@ -330,10 +330,8 @@ def test_band_order_is_output_neutral(gpu, mode):
     only the dispatch order: consecutive multi-frame band launches on one
     stream (the first unordered, the next ones ordered) equal the same bands
     rendered one frame at a time, bit for bit; a change of band geometry on
-    the stream drops the order and still renders right."""
-    import ctypes as C
-
-    import rtamd
+    the stream drops the order and still renders right. The order is opt-in
+    (RTAMD_BAND_ORDER=1); the test switches it on for its launches."""
     from rtamd._lib import lib
     torch = pytest.importorskip("torch")
     from rtamd.workloads import orbit_positions
@@ -343,6 +341,18 @@ def test_band_order_is_output_neutral(gpu, mode):
     S.set_planes(name, mode, s)
     st = torch.cuda.Stream()
     orbit = orbit_positions(64)
+    L.rtx_set_band_order(1)  # opt-in (RTAMD_BAND_ORDER=1)
+    try:
+        _band_order_cases(L, s, name, mode, st, orbit)
+    finally:
+        L.rtx_set_band_order(-1)
+
+
+def _band_order_cases(L, s, name, mode, st, orbit):
+    import ctypes as C
+
+    import rtamd
+    torch = pytest.importorskip("torch")
     for W, H, tile, launches in ((320, 240, rtamd.Tile(8, 1, 4, 0), 4), (256, 200, rtamd.Tile(8, 0, 3, 0), 2),
                                  (320, 240, rtamd.Tile(8, 1, 4, 0), 2)):
         npx = L.rt_tile_pixels(W, H, C.byref(tile))

@@ -99,12 +99,14 @@ struct FrameArgs {
 #ifndef RT_OCT_WAVES
 #define RT_OCT_WAVES 6
 #endif
-// mesh primary: a floor of 4 waves per SIMD (128 VGPRs). The persistent kernel
-// fits it without scratch at leaf batches of 4 triangles (127 VGPRs,
-// RT_LEAF_BATCH_PRIMARY in rt_scenes.h; round 1 needed batches of 2 and still
-// spilled 36 B per lane); a 5-wave floor is slower.
+// mesh primary: a floor of 5 waves per SIMD (102 VGPRs). Built without the SLP
+// vectorizer (Makefile) the persistent kernel takes 96 VGPRs and 36 B of
+// scratch per lane at 5 waves, and is faster than at 4 (117 VGPRs, no
+// scratch): bunny 8 x 2 0.0855 -> 0.0825, the 1.1 M-triangle stand-in 0.3314 ->
+// 0.3149 ms/frame (profiles/r05/slp_ab.txt, two rounds). With SLP on, 5 waves
+// were slower.
 #ifndef RT_MESH_WAVES
-#define RT_MESH_WAVES 4
+#define RT_MESH_WAVES 5
 #endif
 // shading kernels (GENERAL, the reference's default mode): a floor of 4 waves
 // per SIMD. The mesh's takes 135 VGPRs (3 waves) on its own; at 4 it gets 127
@@ -1438,7 +1440,10 @@ int stream_queue(hipStream_t stream, uint32_t **out) {
 // (order_kernel: half-octave cost classes, heaviest first); consecutive orbit
 // frames keep their heavy tiles near the model's outline, so the last launch
 // predicts the next. Output-neutral: only the dispatch order changes.
-// RTAMD_BAND_ORDER=0 switches it off (A/B).
+// Off by default: 8 ranks x 16 frames of bunny / the 1.1 M-triangle stand-in,
+// two interleaved A/B rounds, came out level within the run-to-run spread
+// (profiles/r05/band_order_ab.txt). RTAMD_BAND_ORDER=1 (or rtx_set_band_order)
+// switches it on.
 struct BandSched {
   uint32_t *cost = nullptr, *order = nullptr;
   uint32_t ntiles = 0;
@@ -1446,13 +1451,12 @@ struct BandSched {
 };
 std::map<std::pair<int, hipStream_t>, BandSched> g_band_sched;  // (under g_queue_mu)
 
-bool band_order_enabled() {
-  static const bool on = [] {
-    const char *e = std::getenv("RTAMD_BAND_ORDER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+bool band_order_env() {
+  const char *e = std::getenv("RTAMD_BAND_ORDER");
+  return e && e[0] == '1';
 }
+std::atomic<bool> g_band_order{band_order_env()};
+bool band_order_enabled() { return g_band_order.load(std::memory_order_relaxed); }
 
 int band_sched(hipStream_t stream, uint32_t ntiles, BandSched **out) {
   *out = nullptr;
@@ -2761,9 +2765,6 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
   return RT_OK;
 }
 
-// Diagnostic: persistent launches from now on write per-wave stamps (see
-// PersistQ::stamps) into the device buffer d_buf of cap_waves x 8 u64
-// (d_buf = NULL turns it off). Not part of include/rtamd.h.
 // Row bands with at least this many pixels per frame take the work queue
 // (band_takes_queue); < 0 restores the default threshold.
 int rtx_set_band_queue_px(int64_t px) {
@@ -2771,10 +2772,20 @@ int rtx_set_band_queue_px(int64_t px) {
   return RT_OK;
 }
 
+// Heavy-first band order on (1) / off (0) from now on; < 0 restores the
+// RTAMD_BAND_ORDER setting. Not part of include/rtamd.h.
+int rtx_set_band_order(int on) {
+  g_band_order.store(on < 0 ? band_order_env() : (on != 0));
+  return RT_OK;
+}
+
 // Builder of this thread's last BVH: 1 host, 2 device, 3 host after a failed
 // device build (AUTO mode falls back; see rtx_bvh_inject_failure)
 int rtx_bvh_last_builder(void) { return t_bvh_last; }
 
+// Diagnostic: persistent launches from now on write per-wave stamps (see
+// PersistQ::stamps) into the device buffer d_buf of cap_waves x 8 u64
+// (d_buf = NULL turns it off). Not part of include/rtamd.h.
 int rtx_set_persist_stamps(void *d_buf, int64_t cap_waves) {
   g_persist_stamps = (unsigned long long *)d_buf;
   g_persist_stamps_cap = d_buf ? cap_waves : 0;
