@@ -10,6 +10,8 @@ launch machinery, so numbers are comparable with the bench).
                                             AB_STREAMS: streams per rank, default 2;
                                             AB_GROUP: frames per launch, default 8
   python tools/ab.py modes [workload ...]   primary and default shading
+  python tools/ab.py dropin [workload ...]  rt_render on host buffers (bench.drop_in:
+                                            pageable / pinned, AB_FRAMES frames)
 
 workload: a key of bench.WORKLOADS (bunny, grid, grid_shipped, octree,
 octree_shipped, mesh_large, default_mode: rendered in its own shading mode)
@@ -78,6 +80,9 @@ def main():
                 worst = max(ms for ms, _ in per)
                 print(f"{name} N={n}: max over ranks {worst:.4f} ms/frame -> compute-side bound "
                       f"{base / worst:.2f}x", flush=True)
+        elif what == "dropin":
+            d = bench.drop_in(sc, prm, W, H, frames=int(os.environ.get("AB_FRAMES", "32")))
+            print(f"{name} drop-in: " + ", ".join(f"{k} {v}" for k, v in d.items() if k != "note"), flush=True)
         elif what == "modes":
             for mode in ("primary", "default"):
                 sc.set_plane(None if mode == "primary" else rtamd.Plane((0.0, 1.0, 0.0), off))

@@ -1135,6 +1135,12 @@ __global__ void grp_test_kernel(const float *keys, int n, float *st, uint32_t *s
 }  // namespace
 
 // ================================================================== C ABI ==
+// row bands of rt_render's pageable drop-in path (render_cleared_zero_copy)
+constexpr int kDropBandsMax = 8;
+#ifndef RT_DROPIN_BANDS
+#define RT_DROPIN_BANDS 1
+#endif
+
 struct rt_scene {
   int kind = 0;
   int device = 0;
@@ -1164,8 +1170,11 @@ struct rt_scene {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipStream_t xs[2] = {nullptr, nullptr};  // rt_render: colour / t copy streams (render on xs[0])
   hipEvent_t xev = nullptr;
-  int32_t *d_hit_box = nullptr;  // rt_render: FrameArgs::hit_box of its frame (4 words)
-  int32_t *h_hit_box = nullptr;  // pinned host copy of it
+  // rt_render: FrameArgs::hit_box of its frame (4 words; one per row band of
+  // the pageable drop-in path, kDropBandsMax x 4) and a pinned host copy
+  int32_t *d_hit_box = nullptr;
+  int32_t *h_hit_box = nullptr;
+  hipEvent_t bev[kDropBandsMax] = {};  // the pageable drop-in path: band i's box is on the host
   // rt_render's staging frame for a cleared frame on pageable buffers: pinned
   // host memory the kernel stores its hits into (zero-copy), kept cleared
   uint32_t *stage_c = nullptr;
@@ -1266,8 +1275,10 @@ int ensure_copy_streams(rt_scene *s) {
   for (hipStream_t &x : s->xs)
     if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   if (!s->xev) HIP_TRY(hipEventCreateWithFlags(&s->xev, hipEventDisableTiming));
-  if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, 4 * sizeof(int32_t)));
-  if (!s->h_hit_box) HIP_TRY(hipHostMalloc(&s->h_hit_box, 4 * sizeof(int32_t), hipHostMallocDefault));
+  if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, kDropBandsMax * 4 * sizeof(int32_t)));
+  if (!s->h_hit_box) HIP_TRY(hipHostMalloc(&s->h_hit_box, kDropBandsMax * 4 * sizeof(int32_t), hipHostMallocDefault));
+  for (hipEvent_t &e : s->bev)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return RT_OK;
 }
 
@@ -1305,6 +1316,19 @@ void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool 
     else
       render_kernel<S, MAXD, false, 0><<<fgrid, kFBlock, 0, stream>>>(sc, pl, fa, nullptr);
   }
+}
+
+// The pageable drop-in path's staging frame (render_cleared_zero_copy) back
+// to the heap; the caller has synchronised the streams that use it.
+void stage_free(rt_scene *s) {
+  for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
+    if (*q) {
+      HIP_NOTE(hipHostUnregister(*q));
+      std::free(*q);
+      *q = nullptr;
+    }
+  }
+  s->stage_cap = 0;
 }
 
 // Cost-ordered schedule state for a frame of grid gx x gy blocks on `stream`.
@@ -1355,13 +1379,13 @@ int schedule_end(rt_scene *s, const FrameArgs &fa, uint32_t gx, uint32_t gy, hip
 }
 
 int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
-                  unsigned long long *counters = nullptr, int diag = 0) {
+                  unsigned long long *counters = nullptr, int diag = 0, bool sched = true) {
   FrameArgs fa = fa_in;
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
   const uint32_t gx = (fa.W + kFTile - 1) / kFTile, gy = (fa.rows_local + kFTile - 1) / kFTile;
   fa.order = nullptr;
   fa.cost = nullptr;
-  if (diag == 0) {
+  if (diag == 0 && sched) {
     const int rc = schedule_begin(s, fa, gx, gy, stream);
     if (rc) return rc;
   }
@@ -1394,7 +1418,7 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
     return set_err(RT_E_STATE, "scene has no geometry");
   }
   HIP_TRY(hipGetLastError());
-  if (diag == 0) return schedule_end(s, fa, gx, gy, stream);
+  if (diag == 0 && sched) return schedule_end(s, fa, gx, gy, stream);
   return RT_OK;
 }
 
@@ -2163,8 +2187,9 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->xev) HIP_NOTE(hipEventDestroy(s->xev));
   if (s->d_hit_box) HIP_NOTE(hipFree(s->d_hit_box));
   if (s->h_hit_box) HIP_NOTE(hipHostFree(s->h_hit_box));
-  if (s->stage_c) HIP_NOTE(hipHostFree(s->stage_c));
-  if (s->stage_t) HIP_NOTE(hipHostFree(s->stage_t));
+  for (hipEvent_t e : s->bev)
+    if (e) HIP_NOTE(hipEventDestroy(e));
+  stage_free(s);
   for (hipStream_t x : s->xs)
     if (x) HIP_NOTE(hipStreamDestroy(x));
   HIP_NOTE(hipSetDevice(prev));
@@ -2334,15 +2359,29 @@ bool dropin_zero_copy() {
   return on;
 }
 
+// Row bands of the pageable drop-in path (render_cleared_zero_copy): the
+// frame renders as K contiguous bands on one stream, and the host copies band
+// i's hits while the GPU renders band i + 1. RTAMD_DROPIN_BANDS=K (1..8);
+// rtx_set_dropin_bands sets it at run time (tests).
+int dropin_bands_env() {
+  const char *e = std::getenv("RTAMD_DROPIN_BANDS");
+  const int v = e ? std::atoi(e) : RT_DROPIN_BANDS;
+  return v >= 1 && v <= kDropBandsMax ? v : RT_DROPIN_BANDS;
+}
+std::atomic<int> g_dropin_bands{dropin_bands_env()};
+int dropin_bands() { return g_dropin_bands.load(std::memory_order_relaxed); }
+
 // rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY: the app's
 // frameBuf.clear() + draw, src/main.cpp:197,203): only hit pixels differ from
 // the caller's buffers (raytracing.cpp:91-94), and the kernel stores exactly
-// those -- into HOST memory (zero-copy), so no download follows
-// the kernel:
+// those -- into HOST memory (zero-copy), so no download follows the kernel:
 //  * buffers pinned by rt_host_pin: the hits go straight into them;
 //  * pageable buffers: into the scene's pinned staging frame, which is kept
-//    cleared; after the kernel the host copies the hits' bounding box to the
-//    caller's buffers and clears it in the staging frame again (OpenMP rows).
+//    cleared. The frame renders as dropin_bands() contiguous row bands, one
+//    launch each on one stream, each recording its hits' bounding box; as
+//    each band ends, the host copies its box to the caller's buffers (OpenMP
+//    rows) while the next band renders, and at the end the GPU clears the
+//    boxes in the staging frame again, in stream order before the next frame.
 int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *t, int32_t W, int32_t H,
                              float *ms) {
   const size_t px = (size_t)W * H;
@@ -2358,72 +2397,111 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     }
   } drain{a};
   void *dc = pinned_device_ptr(color, px * 4), *dt = pinned_device_ptr(t, px * 4);
-  const bool direct = dc && dt;
   fa.flags |= RT_FLAG_HITS_ONLY;
   fa.hit_box = nullptr;
-  if (direct) {
+  if (dc && dt) {
     fa.color = (uint32_t *)dc;
     fa.t = (float *)dt;
-  } else {
-    if (px > s->stage_cap) {
-      HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
-      if (s->stage_c) HIP_NOTE(hipHostFree(s->stage_c));
-      if (s->stage_t) HIP_NOTE(hipHostFree(s->stage_t));
-      s->stage_c = nullptr;
-      s->stage_t = nullptr;
-      s->stage_cap = 0;
-      // non-coherent: the GPU may cache the kernel's stores in its L2 until the
-      // kernel's end-of-dispatch release (coherent host memory took the kernel
-      // from 0.195 to 0.280 ms at 1080p); the host reads only after the stream
-      // synchronisation, and the CPU side stays coherent (snooped PCIe writes)
-      HIP_TRY(hipHostMalloc(&s->stage_c, px * 4, hipHostMallocNonCoherent));
-      HIP_TRY(hipHostMalloc(&s->stage_t, px * 4, hipHostMallocNonCoherent));
-      s->stage_cap = px;
-      s->stage_dirty = true;
+    if (g_render_fault.load() > 0) {
+      g_render_fault.fetch_sub(1);
+      return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
     }
-    if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
-      rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
-      s->stage_W = W;
-      s->stage_H = H;
-      s->stage_dirty = false;
-    }
-    void *sc = nullptr, *st = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
-    HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
-    fa.color = (uint32_t *)sc;
-    fa.t = (float *)st;
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_hit_box, 0x7FFFFFFF, 4, a));
-    fa.hit_box = s->d_hit_box;
+    HIP_TRY(hipEventRecord(s->ev0, a));
+    if (int rc = launch_render(s, fa, a)) return rc;
+    HIP_TRY(hipEventRecord(s->ev1, a));
+    HIP_TRY(hipStreamSynchronize(a));
+    if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    return RT_OK;
   }
+  if (px > s->stage_cap) {
+    HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
+    stage_free(s);
+    // page-aligned host memory registered with the runtime (as rt_host_pin
+    // does for the caller's buffers): the kernel's stores into it cost what
+    // they cost into the caller's pinned frame (1080p bunny 0.199 ms), where
+    // hipHostMalloc'ed staging, coherent or hipHostMallocNonCoherent, took
+    // 0.28 ms
+    const size_t bytes = (px * 4 + 4095) & ~(size_t)4095;
+    for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
+      *q = std::aligned_alloc(4096, bytes);
+      if (!*q) {
+        stage_free(s);
+        return set_err(RT_E_DEVICE, "staging frame: out of host memory");
+      }
+      if (const hipError_t e = hipHostRegister(*q, bytes, hipHostRegisterMapped)) {
+        std::free(*q);
+        *q = nullptr;
+        stage_free(s);
+        return set_err(RT_E_DEVICE, std::string("staging frame: ") + hipGetErrorString(e));
+      }
+    }
+    s->stage_cap = px;
+    s->stage_dirty = true;
+  }
+  if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
+    rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
+    s->stage_W = W;
+    s->stage_H = H;
+    s->stage_dirty = false;
+  }
+  void *sc = nullptr, *st = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
+  HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
+  // K contiguous bands of R rows (a multiple of the 8-row wave tile); band i
+  // is rank i of a K-rank tile, its packed rows land at their own image rows
+  // when its buffers start at row i * R
+  int K = std::min(dropin_bands(), (H + 7) / 8);
+  const int32_t R = (((H + K - 1) / K) + 7) & ~7;
+  K = (H + R - 1) / R;
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_hit_box, 0x7FFFFFFF, 4 * K, a));
   if (g_render_fault.load() > 0) {
     g_render_fault.fetch_sub(1);
     return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
   }
   HIP_TRY(hipEventRecord(s->ev0, a));
-  if (!direct) s->stage_dirty = true;  // until its box is cleared again below
-  if (int rc = launch_render(s, fa, a)) return rc;
-  HIP_TRY(hipEventRecord(s->ev1, a));
-  if (!direct) HIP_TRY(hipMemcpyAsync(s->h_hit_box, s->d_hit_box, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, a));
-  HIP_TRY(hipStreamSynchronize(a));
-  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
-  if (!direct) {
-    const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
-    if (x0 <= x1 && y0 <= y1) {
-      // the hits' box to the caller (host threads), then the same box of the
-      // staging frame cleared again by the GPU, in stream order before the
-      // next frame's kernel; the call does not wait for it
-      rth::copy_rect(color, t, s->stage_c, s->stage_t, W, x0, x1, y0, y1, y1 - y0 >= 32 ? 8 : 1);
-      drain.on = false;
-      void *sc = nullptr, *st = nullptr;
-      HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
-      HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
-      const int32_t w = x1 - x0 + 1;
-      clear_rect_kernel<<<dim3((unsigned)((w + 255) / 256), (unsigned)(y1 - y0 + 1)), 256, 0, a>>>(
-          (uint32_t *)sc, (float *)st, W, x0, x1, y0);
-      HIP_TRY(hipGetLastError());
+  s->stage_dirty = true;  // until its boxes are cleared again below
+  for (int i = 0; i < K; ++i) {
+    FrameArgs fb = fa;
+    if (K > 1) {
+      fb.band_rows = R;
+      fb.rank = i;
+      fb.nranks = K;
+      fb.rows_local = std::min(R, H - i * R);
     }
-    s->stage_dirty = false;
+    fb.color = (uint32_t *)sc + (size_t)i * R * W;
+    fb.t = (float *)st + (size_t)i * R * W;
+    fb.hit_box = s->d_hit_box + 4 * i;
+    // one band: the frame's cost-ordered schedule; several: blockIdx order
+    if (int rc = launch_render(s, fb, a, nullptr, 0, K == 1)) return rc;
+    if (i == K - 1) HIP_TRY(hipEventRecord(s->ev1, a));
+    HIP_TRY(hipMemcpyAsync(s->h_hit_box + 4 * i, s->d_hit_box + 4 * i, 4 * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, a));
+    HIP_TRY(hipEventRecord(s->bev[i], a));
   }
+  int32_t ux0 = INT32_MAX, ux1 = -1, uy0 = INT32_MAX, uy1 = -1;  // union of the bands' boxes
+  for (int i = 0; i < K; ++i) {
+    HIP_TRY(hipEventSynchronize(s->bev[i]));
+    const int32_t *b = s->h_hit_box + 4 * i;
+    const int32_t x0 = b[0], x1 = -b[1], y0 = b[2], y1 = -b[3];
+    if (x0 > x1 || y0 > y1) continue;  // no hit in this band
+    // the box's rows in the image: band-local row y -> i * R + y
+    rth::copy_rect(color, t, s->stage_c, s->stage_t, W, x0, x1, i * R + y0, i * R + y1, 0);
+    ux0 = std::min(ux0, x0);
+    ux1 = std::max(ux1, x1);
+    uy0 = std::min(uy0, i * R + y0);
+    uy1 = std::max(uy1, i * R + y1);
+  }
+  if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  if (ux0 <= ux1) {
+    // the staging frame's hit pixels cleared again by the GPU, in stream order
+    // before the next frame's kernel; the call does not wait for it
+    drain.on = false;
+    const int32_t w = ux1 - ux0 + 1;
+    clear_rect_kernel<<<dim3((unsigned)((w + 255) / 256), (unsigned)(uy1 - uy0 + 1)), 256, 0, a>>>(
+        (uint32_t *)sc, (float *)st, W, ux0, ux1, uy0);
+    HIP_TRY(hipGetLastError());
+  }
+  s->stage_dirty = false;
   return RT_OK;
 }
 
@@ -2769,6 +2847,14 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // (band_takes_queue); < 0 restores the default threshold.
 int rtx_set_band_queue_px(int64_t px) {
   g_band_queue_px.store(px < 0 ? (int64_t)1000000 : px);
+  return RT_OK;
+}
+
+// Row bands of rt_render's pageable drop-in path from now on (1..8); <= 0
+// restores the RTAMD_DROPIN_BANDS setting. Not part of include/rtamd.h.
+int rtx_set_dropin_bands(int k) {
+  if (k > kDropBandsMax) return set_err(RT_E_INVALID, "at most 8 drop-in bands");
+  g_dropin_bands.store(k <= 0 ? dropin_bands_env() : k);
   return RT_OK;
 }
 

@@ -1011,6 +1011,8 @@ void camera_matrices(const float pos[3], const float target[3], const float up[3
 void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t x0, int32_t x1,
                int32_t y0, int32_t y1, int threads) {
   const size_t w = (size_t)(x1 - x0 + 1);
+  if (threads <= 0)  // one thread per 32 rows, at most the OpenMP default and 16
+    threads = std::max(1, std::min({(y1 - y0 + 1) / 32, omp_get_max_threads(), 16}));
 #pragma omp parallel for schedule(static) num_threads(threads) if (threads > 1)
   for (int32_t y = y0; y <= y1; ++y) {
     const size_t o = (size_t)y * (size_t)W + (size_t)x0;

@@ -175,7 +175,8 @@ void camera_matrices(const float pos[3], const float target[3], const float up[3
 
 // rt_render's staged download of a cleared frame: rows [y0, y1] x columns
 // [x0, x1] of two W-wide frames copied from the staging frame (sc, st) to the
-// caller's buffers (dc, dt); rows split over up to `threads` OpenMP threads.
+// caller's buffers (dc, dt); rows split over up to `threads` OpenMP threads
+// (<= 0: one per 32 rows, at most the OpenMP default and 16).
 void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t x0, int32_t x1,
                int32_t y0, int32_t y1, int threads);
 // FrameBuffer::clear() of n pixels (0, +inf), over up to `threads` threads.
