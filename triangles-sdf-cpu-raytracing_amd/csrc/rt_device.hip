@@ -334,6 +334,13 @@ __device__ __forceinline__ void fb_store(T *p, T v, bool peer) {
 // A per-wave system-scope fence there costs an L2 write-back per wave: the
 // one-frame kernel's 32 k waves took the frame from 0.19 to ~0.38 ms.)
 constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL;
+// Internal flag (never passed through the C ABI; fill_frame rejects it): the
+// frame lives in host memory (rt_render's zero-copy cleared frames) and takes
+// system-scope stores, which write through this GPU's L2, with no per-wave
+// fence. Agent-scope stores leave the lines dirty in L2 for the end-of-kernel
+// release to write back over PCIe after the last wave; RTAMD_HOST_STORES=agent
+// keeps those (A/B switch).
+constexpr uint32_t kFlagHostFrame = 1u << 30;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
   if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -399,6 +406,7 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
     // full frame's own row (a peer's frame mapped over xGMI)
     const bool peer = (fa.flags & kSysStoreFlags) != 0;
+    const bool sys = (fa.flags & (kSysStoreFlags | kFlagHostFrame)) != 0;
     const int yb = peer ? yo : yl;
     // 32-bit pixel index (check_params caps W*H at 2^31): one register live
     // across the traversal instead of two
@@ -430,11 +438,11 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     if (!active) {
       // helper lane of the cooperative path: no pixel of its own
     } else if (clear && !hits_only) {
-      fb_store(fa.color + idx, store ? pack_rgba(c) : 0u, peer);
-      fb_store(fa.t + idx, store ? t : kInf, peer);
+      fb_store(fa.color + idx, store ? pack_rgba(c) : 0u, sys);
+      fb_store(fa.t + idx, store ? t : kInf, sys);
     } else if (store) {
-      fb_store(fa.color + idx, pack_rgba(c), peer);
-      fb_store(fa.t + idx, t, peer);
+      fb_store(fa.color + idx, pack_rgba(c), sys);
+      fb_store(fa.t + idx, t, sys);
     }
     return active && store;
   }
@@ -2359,6 +2367,16 @@ bool dropin_zero_copy() {
   return on;
 }
 
+// System-scope stores into host frames (kFlagHostFrame); RTAMD_HOST_STORES=agent
+// turns them off (A/B switch).
+bool host_sys_stores() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_HOST_STORES");
+    return !(e && std::strcmp(e, "agent") == 0);
+  }();
+  return on;
+}
+
 // Row bands of the pageable drop-in path (render_cleared_zero_copy): the
 // frame renders as K contiguous bands on one stream, and the host copies band
 // i's hits while the GPU renders band i + 1. RTAMD_DROPIN_BANDS=K (1..8);
@@ -2397,7 +2415,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     }
   } drain{a};
   void *dc = pinned_device_ptr(color, px * 4), *dt = pinned_device_ptr(t, px * 4);
-  fa.flags |= RT_FLAG_HITS_ONLY;
+  fa.flags |= RT_FLAG_HITS_ONLY | (host_sys_stores() ? kFlagHostFrame : 0u);
   fa.hit_box = nullptr;
   if (dc && dt) {
     fa.color = (uint32_t *)dc;
