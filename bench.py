@@ -224,6 +224,9 @@ def stream_pool(k):
     return _POOL[:k]
 
 
+LAST_RUN = {}
+
+
 def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=1):
     """Full frames (or one rank's row bands with `tile`), render kernel only.
     Frames go out in launches of up to `batch` frames (rt_render_device_frames);
@@ -270,10 +273,12 @@ def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=
         t0 = time.perf_counter()
         for j, (k, n) in enumerate(timed):
             issue(j, params[k:k + n], evs[j])
+        t_issued = time.perf_counter()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
     finally:
         gc.enable()
+    LAST_RUN["issue_s"] = t_issued - t0  # host time to issue the timed launches (tools/ab.py)
     launches = [(a.elapsed_time(b), n) for (a, b), (_, n) in zip(evs, timed)]
     jl, (kl, nl) = len(timed) - 1, timed[-1]
     return wall, launches, bufs[jl % inflight][nl - 1]

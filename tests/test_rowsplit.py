@@ -290,36 +290,29 @@ def test_drop_in_failure_leaves_no_copy_in_flight(gpu):
     assert np.array_equal(c, rc)
 
 
-@pytest.mark.parametrize("pinned,bands", [(False, 1), (False, 3), (False, 8), (True, 1)])
-def test_drop_in_cleared_frames_zero_copy(gpu, pinned, bands):
+@pytest.mark.parametrize("pinned", [False, True])
+def test_drop_in_cleared_frames_zero_copy(gpu, pinned):
     """rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY, the
     app's frameBuf.clear() + draw) stores the hits straight into HOST memory:
     into the caller's buffers when rt_host_pin pinned them, else into the
-    scene's pinned staging frame, rendered as `bands` contiguous row bands
-    whose hit boxes are copied to the caller as each band ends and cleared
-    again. A sequence of frames -- cameras with narrow, wide and no hits, a
-    size change, default and primary shading, an injected failure -- each
-    equals the same frame through the device-frame path (RT_FLAG_CLEAR alone:
-    every pixel written on the device and downloaded)."""
+    scene's pinned staging frame, whose per-row spans of stored pixels are
+    then copied to the caller and cleared again. A sequence of frames --
+    cameras with narrow, wide and no hits, size changes (a taller frame
+    regrows the span buffers), default and primary shading, an injected
+    failure -- each equals the same frame through the device-frame path
+    (RT_FLAG_CLEAR alone: every pixel written on the device and downloaded)."""
     import ctypes as C
     rt = gpu
     L = rt.lib()
     L.rtx_render_inject_failure.argtypes = [C.c_int32]
-    rt._lib.check(L.rtx_set_dropin_bands(bands))
-    try:
-        _drop_in_cleared_sequence(rt, L, pinned)
-    finally:
-        L.rtx_set_dropin_bands(0)
-
-
-def _drop_in_cleared_sequence(rt, L, pinned):
     name = "stanford-bunny.obj"
     sc = S.gpu_scene(name)
     seq = [(320, 180, "default", (0.0, 0.3, 2.5)), (320, 180, "primary", (0.0, 0.1, 3.5)),
            (320, 180, "primary", (0.2, 0.1, 0.9)), (320, 180, "default", (0.0, 0.0, -30.0)),
            (200, 120, "default", (1.2, 0.4, 1.9)), ("fail", None, None, None),
            (320, 180, "primary", (-0.7, 0.5, 2.2)), (200, 120, "default", (0.4, -0.1, 2.6)),
-           (203, 61, "default", (0.1, 0.2, 2.4))]
+           (203, 61, "default", (0.1, 0.2, 2.4)), (160, 240, "primary", (0.3, 0.0, 2.0)),
+           (320, 180, "default", (0.0, 0.3, 2.5))]
     bufs = {}
     try:
         for W, H, mode, pos in seq:

@@ -85,7 +85,10 @@ struct FrameArgs {
   uint32_t *cost;         // per-tile cost of this frame (shader cycles, max over waves), or NULL
   // one-frame kernel: bounding box of the pixels a hit was stored to, as
   // (min x, -max x, min y, -max y) in buffer coordinates (four atomicMin
-  // words, initialised to INT32_MAX), or NULL (rt_render's partial download)
+  // words, initialised to INT32_MAX), or NULL (rt_render's partial download).
+  // With kFlagRowSpan in flags: per buffer row instead, the span of those
+  // pixels as (min x, -max x), two such words per row (rt_render's zero-copy
+  // cleared frames on pageable buffers: the host copies just these spans)
   int32_t *hit_box;
 };
 
@@ -341,6 +344,8 @@ constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL;
 // release to write back over PCIe after the last wave; RTAMD_HOST_STORES=agent
 // keeps those (A/B switch).
 constexpr uint32_t kFlagHostFrame = 1u << 30;
+// Internal flag: FrameArgs::hit_box holds per-row spans (see FrameArgs).
+constexpr uint32_t kFlagRowSpan = 1u << 29;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
   if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -467,7 +472,7 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
   const int yl = BT == 64 ? (int)by * 8 + (lane >> 3) : (int)by * kTile + (wave >> 1) * 8 + (lane >> 3);
   const bool stored = render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, xo, yl);
   if constexpr (DIAG == 0) {
-    if (fa.hit_box && __ballot(stored)) {  // this wave's stored pixels into the frame's hit box
+    if (fa.hit_box && !(fa.flags & kFlagRowSpan) && __ballot(stored)) {  // this wave's stored pixels into the frame's hit box
       int32_t v[4] = {stored ? xo : INT32_MAX, stored ? -xo : INT32_MAX, stored ? yl : INT32_MAX,
                       stored ? -yl : INT32_MAX};
 #pragma unroll
@@ -477,9 +482,27 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
           const int32_t o = __shfl_xor(v[i], off, 64);
           v[i] = o < v[i] ? o : v[i];
         }
+      // one lane, and only the words this wave improves: ~30 k waves' atomics
+      // on one cache line would queue behind each other at the L2
       if (lane == __ffsll((unsigned long long)__ballot(1)) - 1)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicMin(fa.hit_box + i, v[i]);
+        for (int i = 0; i < 4; ++i)
+          if (v[i] < __hip_atomic_load(fa.hit_box + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(fa.hit_box + i, v[i]);
+    }
+    if (fa.hit_box && (fa.flags & kFlagRowSpan) && __ballot(stored)) {  // per row of the tile: its stored pixels' span
+      int32_t lo = stored ? xo : INT32_MAX, nhi = stored ? -xo : INT32_MAX;
+#pragma unroll
+      for (int off = 1; off < 8; off <<= 1) {  // the 8 lanes of one tile row
+        const int32_t a = __shfl_xor(lo, off, 64), b = __shfl_xor(nhi, off, 64);
+        lo = a < lo ? a : lo;
+        nhi = b < nhi ? b : nhi;
+      }
+      if ((lane & 7) == 0 && lo != INT32_MAX) {
+        int32_t *sp = fa.hit_box + 2 * yl;
+        if (lo < __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(sp, lo);
+        if (nhi < __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(sp + 1, nhi);
+      }
     }
   }
   if constexpr (DIAG == 0) {
@@ -1051,15 +1074,25 @@ __global__ void clear_kernel(uint32_t *c, float *t, int64_t n) {
   }
 }
 
-// FrameBuffer::clear() of the rectangle [x0, x1] x [y0, y1] of a W-wide frame
-// (rt_render's staging frame, after its hit box was copied out): one thread
-// per pixel, blockIdx.y = row.
-__global__ void clear_rect_kernel(uint32_t *c, float *t, int32_t W, int32_t x0, int32_t x1, int32_t y0) {
-  const int32_t x = x0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (x > x1) return;
-  const size_t i = (size_t)(y0 + (int32_t)blockIdx.y) * (size_t)W + (size_t)x;
-  c[i] = 0u;
-  t[i] = kInf;
+// rt_render's hit box / row spans (n words) to their pinned, mapped host
+// copy: system-scope stores, which the host reads after synchronising the
+// stream (a kernel in stream order instead of a small DMA copy)
+__global__ void box_out_kernel(const int32_t *d_box, int32_t *h_box, int n) {
+  for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < n; i += (int)(gridDim.x * blockDim.x))
+    __hip_atomic_store(h_box + i, d_box[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the staging frame's stored spans (the row spans of its last frame) cleared
+// again: block y clears row y's span. A row without hits holds (INT32_MAX,
+// INT32_MAX): it returns before any index is formed from them.
+__global__ void clear_spans_kernel(uint32_t *c, float *t, const int32_t *span, int32_t W) {
+  const int32_t y = (int32_t)blockIdx.x, lo = span[2 * y], hi = -span[2 * y + 1];
+  if (lo > hi || lo < 0 || hi >= W) return;
+  for (int32_t x = lo + (int32_t)threadIdx.x; x <= hi; x += (int32_t)blockDim.x) {
+    const size_t i = (size_t)y * (size_t)W + (size_t)x;
+    c[i] = 0u;
+    t[i] = kInf;
+  }
 }
 
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
@@ -1143,12 +1176,6 @@ __global__ void grp_test_kernel(const float *keys, int n, float *st, uint32_t *s
 }  // namespace
 
 // ================================================================== C ABI ==
-// row bands of rt_render's pageable drop-in path (render_cleared_zero_copy)
-constexpr int kDropBandsMax = 8;
-#ifndef RT_DROPIN_BANDS
-#define RT_DROPIN_BANDS 1
-#endif
-
 struct rt_scene {
   int kind = 0;
   int device = 0;
@@ -1178,11 +1205,17 @@ struct rt_scene {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipStream_t xs[2] = {nullptr, nullptr};  // rt_render: colour / t copy streams (render on xs[0])
   hipEvent_t xev = nullptr;
-  // rt_render: FrameArgs::hit_box of its frame (4 words; one per row band of
-  // the pageable drop-in path, kDropBandsMax x 4) and a pinned host copy
+  // rt_render: FrameArgs::hit_box of its frame (4 words) and a pinned,
+  // mapped host copy (h_hit_box_dev: its device address, box_out_kernel)
   int32_t *d_hit_box = nullptr;
   int32_t *h_hit_box = nullptr;
-  hipEvent_t bev[kDropBandsMax] = {};  // the pageable drop-in path: band i's box is on the host
+  int32_t *h_hit_box_dev = nullptr;
+  // the pageable zero-copy path: FrameArgs::row_span (2 words per row) and its
+  // pinned, mapped host copy, for span_cap rows
+  int32_t *d_row_span = nullptr;
+  int32_t *h_row_span = nullptr;
+  int32_t *h_row_span_dev = nullptr;
+  int32_t span_cap = 0;
   // rt_render's staging frame for a cleared frame on pageable buffers: pinned
   // host memory the kernel stores its hits into (zero-copy), kept cleared
   uint32_t *stage_c = nullptr;
@@ -1283,10 +1316,11 @@ int ensure_copy_streams(rt_scene *s) {
   for (hipStream_t &x : s->xs)
     if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   if (!s->xev) HIP_TRY(hipEventCreateWithFlags(&s->xev, hipEventDisableTiming));
-  if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, kDropBandsMax * 4 * sizeof(int32_t)));
-  if (!s->h_hit_box) HIP_TRY(hipHostMalloc(&s->h_hit_box, kDropBandsMax * 4 * sizeof(int32_t), hipHostMallocDefault));
-  for (hipEvent_t &e : s->bev)
-    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, 4 * sizeof(int32_t)));
+  if (!s->h_hit_box) {
+    HIP_TRY(hipHostMalloc(&s->h_hit_box, 4 * sizeof(int32_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void **)&s->h_hit_box_dev, s->h_hit_box, 0));
+  }
   return RT_OK;
 }
 
@@ -2195,8 +2229,8 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->xev) HIP_NOTE(hipEventDestroy(s->xev));
   if (s->d_hit_box) HIP_NOTE(hipFree(s->d_hit_box));
   if (s->h_hit_box) HIP_NOTE(hipHostFree(s->h_hit_box));
-  for (hipEvent_t e : s->bev)
-    if (e) HIP_NOTE(hipEventDestroy(e));
+  if (s->d_row_span) HIP_NOTE(hipFree(s->d_row_span));
+  if (s->h_row_span) HIP_NOTE(hipHostFree(s->h_row_span));
   stage_free(s);
   for (hipStream_t x : s->xs)
     if (x) HIP_NOTE(hipStreamDestroy(x));
@@ -2377,18 +2411,6 @@ bool host_sys_stores() {
   return on;
 }
 
-// Row bands of the pageable drop-in path (render_cleared_zero_copy): the
-// frame renders as K contiguous bands on one stream, and the host copies band
-// i's hits while the GPU renders band i + 1. RTAMD_DROPIN_BANDS=K (1..8);
-// rtx_set_dropin_bands sets it at run time (tests).
-int dropin_bands_env() {
-  const char *e = std::getenv("RTAMD_DROPIN_BANDS");
-  const int v = e ? std::atoi(e) : RT_DROPIN_BANDS;
-  return v >= 1 && v <= kDropBandsMax ? v : RT_DROPIN_BANDS;
-}
-std::atomic<int> g_dropin_bands{dropin_bands_env()};
-int dropin_bands() { return g_dropin_bands.load(std::memory_order_relaxed); }
-
 // rt_render of a cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY: the app's
 // frameBuf.clear() + draw, src/main.cpp:197,203): only hit pixels differ from
 // the caller's buffers (raytracing.cpp:91-94), and the kernel stores exactly
@@ -2434,11 +2456,8 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   if (px > s->stage_cap) {
     HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
     stage_free(s);
-    // page-aligned host memory registered with the runtime (as rt_host_pin
-    // does for the caller's buffers): the kernel's stores into it cost what
-    // they cost into the caller's pinned frame (1080p bunny 0.199 ms), where
-    // hipHostMalloc'ed staging, coherent or hipHostMallocNonCoherent, took
-    // 0.28 ms
+    // page-aligned host memory registered with the runtime, mapped (as
+    // rt_host_pin does for the caller's buffers)
     const size_t bytes = (px * 4 + 4095) & ~(size_t)4095;
     for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
       *q = std::aligned_alloc(4096, bytes);
@@ -2456,69 +2475,52 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     s->stage_cap = px;
     s->stage_dirty = true;
   }
+  void *sc = nullptr, *st = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
+  HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
+  if (H > s->span_cap) {
+    HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's span clear reads d_row_span)
+    if (s->d_row_span) HIP_NOTE(hipFree(s->d_row_span));
+    if (s->h_row_span) HIP_NOTE(hipHostFree(s->h_row_span));
+    s->d_row_span = s->h_row_span = s->h_row_span_dev = nullptr;
+    s->span_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_row_span, (size_t)H * 2 * sizeof(int32_t)));
+    HIP_TRY(hipHostMalloc(&s->h_row_span, (size_t)H * 2 * sizeof(int32_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void **)&s->h_row_span_dev, s->h_row_span, 0));
+    s->span_cap = H;
+    s->stage_dirty = true;  // (the spans of the frame in the staging frame are gone)
+  }
   if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
     rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
     s->stage_W = W;
     s->stage_H = H;
     s->stage_dirty = false;
   }
-  void *sc = nullptr, *st = nullptr;
-  HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
-  HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
-  // K contiguous bands of R rows (a multiple of the 8-row wave tile); band i
-  // is rank i of a K-rank tile, its packed rows land at their own image rows
-  // when its buffers start at row i * R
-  int K = std::min(dropin_bands(), (H + 7) / 8);
-  const int32_t R = (((H + K - 1) / K) + 7) & ~7;
-  K = (H + R - 1) / R;
-  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_hit_box, 0x7FFFFFFF, 4 * K, a));
+  fa.color = (uint32_t *)sc;
+  fa.t = (float *)st;
+  fa.hit_box = s->d_row_span;
+  fa.flags |= kFlagRowSpan;
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_row_span, 0x7FFFFFFF, (size_t)H * 2, a));
   if (g_render_fault.load() > 0) {
     g_render_fault.fetch_sub(1);
     return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
   }
   HIP_TRY(hipEventRecord(s->ev0, a));
-  s->stage_dirty = true;  // until its boxes are cleared again below
-  for (int i = 0; i < K; ++i) {
-    FrameArgs fb = fa;
-    if (K > 1) {
-      fb.band_rows = R;
-      fb.rank = i;
-      fb.nranks = K;
-      fb.rows_local = std::min(R, H - i * R);
-    }
-    fb.color = (uint32_t *)sc + (size_t)i * R * W;
-    fb.t = (float *)st + (size_t)i * R * W;
-    fb.hit_box = s->d_hit_box + 4 * i;
-    // one band: the frame's cost-ordered schedule; several: blockIdx order
-    if (int rc = launch_render(s, fb, a, nullptr, 0, K == 1)) return rc;
-    if (i == K - 1) HIP_TRY(hipEventRecord(s->ev1, a));
-    HIP_TRY(hipMemcpyAsync(s->h_hit_box + 4 * i, s->d_hit_box + 4 * i, 4 * sizeof(int32_t),
-                           hipMemcpyDeviceToHost, a));
-    HIP_TRY(hipEventRecord(s->bev[i], a));
-  }
-  int32_t ux0 = INT32_MAX, ux1 = -1, uy0 = INT32_MAX, uy1 = -1;  // union of the bands' boxes
-  for (int i = 0; i < K; ++i) {
-    HIP_TRY(hipEventSynchronize(s->bev[i]));
-    const int32_t *b = s->h_hit_box + 4 * i;
-    const int32_t x0 = b[0], x1 = -b[1], y0 = b[2], y1 = -b[3];
-    if (x0 > x1 || y0 > y1) continue;  // no hit in this band
-    // the box's rows in the image: band-local row y -> i * R + y
-    rth::copy_rect(color, t, s->stage_c, s->stage_t, W, x0, x1, i * R + y0, i * R + y1, 0);
-    ux0 = std::min(ux0, x0);
-    ux1 = std::max(ux1, x1);
-    uy0 = std::min(uy0, i * R + y0);
-    uy1 = std::max(uy1, i * R + y1);
-  }
+  s->stage_dirty = true;  // until its spans are cleared again below
+  if (int rc = launch_render(s, fa, a)) return rc;
+  HIP_TRY(hipEventRecord(s->ev1, a));
+  box_out_kernel<<<(unsigned)((2 * H + 255) / 256), 256, 0, a>>>(s->d_row_span, s->h_row_span_dev, 2 * H);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(a));
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
-  if (ux0 <= ux1) {
-    // the staging frame's hit pixels cleared again by the GPU, in stream order
-    // before the next frame's kernel; the call does not wait for it
-    drain.on = false;
-    const int32_t w = ux1 - ux0 + 1;
-    clear_rect_kernel<<<dim3((unsigned)((w + 255) / 256), (unsigned)(uy1 - uy0 + 1)), 256, 0, a>>>(
-        (uint32_t *)sc, (float *)st, W, ux0, ux1, uy0);
-    HIP_TRY(hipGetLastError());
-  }
+  // the stored spans to the caller (host threads; every other pixel of the
+  // caller's cleared frame already holds the staging frame's 0 / +inf), then
+  // the same spans of the staging frame cleared again by the GPU, in stream
+  // order before the next frame's kernel; the call does not wait for it
+  rth::copy_spans(color, t, s->stage_c, s->stage_t, W, H, s->h_row_span, 0);
+  drain.on = false;
+  clear_spans_kernel<<<(unsigned)H, 256, 0, a>>>((uint32_t *)sc, (float *)st, s->d_row_span, W);
+  HIP_TRY(hipGetLastError());
   s->stage_dirty = false;
   return RT_OK;
 }
@@ -2589,7 +2591,8 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
     HIP_TRY(hipMemcpyAsync(t, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
     HIP_TRY(hipMemcpyAsync(color, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
   } else {
-    HIP_TRY(hipMemcpyAsync(s->h_hit_box, s->d_hit_box, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, a));
+    box_out_kernel<<<1, 64, 0, a>>>(s->d_hit_box, s->h_hit_box_dev, 4);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(a));
     const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
     if (x0 <= x1 && y0 <= y1) {  // else: no hit, nothing changed
@@ -2865,14 +2868,6 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // (band_takes_queue); < 0 restores the default threshold.
 int rtx_set_band_queue_px(int64_t px) {
   g_band_queue_px.store(px < 0 ? (int64_t)1000000 : px);
-  return RT_OK;
-}
-
-// Row bands of rt_render's pageable drop-in path from now on (1..8); <= 0
-// restores the RTAMD_DROPIN_BANDS setting. Not part of include/rtamd.h.
-int rtx_set_dropin_bands(int k) {
-  if (k > kDropBandsMax) return set_err(RT_E_INVALID, "at most 8 drop-in bands");
-  g_dropin_bands.store(k <= 0 ? dropin_bands_env() : k);
   return RT_OK;
 }
 

@@ -1021,6 +1021,19 @@ void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int
   }
 }
 
+void copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
+                const int32_t *span, int threads) {
+  if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), 16}));
+#pragma omp parallel for schedule(static) num_threads(threads) if (threads > 1)
+  for (int32_t y = 0; y < H; ++y) {
+    const int32_t lo = span[2 * y], hi = -span[2 * y + 1];
+    if (lo > hi || lo < 0 || hi >= W) continue;  // (no hit: INT32_MAX, INT32_MAX)
+    const size_t o = (size_t)y * (size_t)W + (size_t)lo, w = (size_t)(hi - lo + 1);
+    std::memcpy(dc + o, sc + o, w * 4);
+    std::memcpy(dt + o, st + o, w * 4);
+  }
+}
+
 void clear_frame(uint32_t *c, float *t, int64_t n, int threads) {
   const float inf = std::numeric_limits<float>::infinity();
   const int64_t chunk = 1 << 16;

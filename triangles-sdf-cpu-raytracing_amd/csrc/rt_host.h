@@ -179,6 +179,11 @@ void camera_matrices(const float pos[3], const float target[3], const float up[3
 // (<= 0: one per 32 rows, at most the OpenMP default and 16).
 void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t x0, int32_t x1,
                int32_t y0, int32_t y1, int threads);
+// The same for per-row spans: row y's columns [span[2y], -span[2y+1]] (rows
+// with span[2y] > -span[2y+1] are skipped); rt_render's zero-copy cleared
+// frames on pageable buffers (FrameArgs::row_span).
+void copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
+                const int32_t *span, int threads);
 // FrameBuffer::clear() of n pixels (0, +inf), over up to `threads` threads.
 void clear_frame(uint32_t *c, float *t, int64_t n, int threads);
 
