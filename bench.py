@@ -263,6 +263,9 @@ def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=
         issue(j, [params[(k + i) % len(params)] for i in range(n)])
     timed = split_launches(warmup, steps, batch)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
+    for j, (a, b) in enumerate(evs):  # a torch event creates its HIP event at its first record: here, untimed
+        a.record(streams[j % inflight])
+        b.record(streams[j % inflight])
     # no garbage-collector pass inside the timed region: a full collection of this
     # process's heap (torch, numpy, ctypes) stalls the host thread that issues the
     # launches for milliseconds, longer than the 20-frame run itself

@@ -58,6 +58,9 @@ class HostDevice:
     def wait_event(self, st, ev):
         return None
 
+    def release_event(self, ev):
+        return None
+
     def sync_stream(self, st):
         return None
 

@@ -86,6 +86,7 @@ class HipDevice:
 
     def __init__(self):
         self.tensor_device = torch.device("cuda", torch.cuda.current_device())
+        self._free_events = []
 
     # streams and events
     def stream(self):
@@ -95,9 +96,15 @@ class HipDevice:
         return torch.cuda.stream(st)
 
     def event(self, st):
-        ev = torch.cuda.Event()
+        # recycled events (release_event): a fresh torch event creates its HIP
+        # event lazily at its first record, inside the caller's issue loop
+        ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
         ev.record(st)
         return ev
+
+    def release_event(self, ev):
+        """ev's last wait is enqueued: it may be recorded again."""
+        self._free_events.append(ev)
 
     def wait_event(self, st, ev):
         st.wait_event(ev)
@@ -302,7 +309,9 @@ class RowSplitRenderer:
     def _p2p_group(self, g: int, params, st):
         frames = range(g * self.G, g * self.G + len(params))
         if self.rank == 0 and g >= self.D:
-            self.dv.wait_event(st, self.ev_clear.pop(g - self.D))
+            ev = self.ev_clear.pop(g - self.D)
+            self.dv.wait_event(st, ev)
+            self.dv.release_event(ev)
         if self.rank != 0 and g >= self.D - 1:
             self.works[g - self.D + 1].wait()  # (current stream = st)
         cp, tp = zip(*(self._slot_ptrs(self._mapped, k % self.S) for k in frames))
