@@ -227,6 +227,27 @@ def stream_pool(k):
 LAST_RUN = {}
 
 
+class NoGC:
+    """No garbage-collector pass inside a timed region: a full collection of
+    this process's heap (torch, numpy, ctypes) stalls the host thread that
+    issues the launches for milliseconds, longer than the 20-frame run itself.
+    The collection runs on entry, before the region's warm-up: run right
+    before t0 it left the first timed launch's issue ~120 us slower (bunny
+    bands, tools/issue_probe2.py), 0.13 ms of the 20-frame wall. Nested uses
+    leave the collector off."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        if self.was:
+            gc.collect()
+            gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+
+
 def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=1):
     """Full frames (or one rank's row bands with `tile`), render kernel only.
     Frames go out in launches of up to `batch` frames (rt_render_device_frames);
@@ -259,29 +280,25 @@ def run_single(scene, params, warmup, steps, W, H, inflight=2, tile=None, batch=
                 ev[1].record(st)
 
     nwarm = max(warmup, inflight * batch)
-    for j, (k, n) in enumerate(split_launches(0, nwarm, batch)):
-        issue(j, [params[(k + i) % len(params)] for i in range(n)])
-    timed = split_launches(warmup, steps, batch)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
-    for j, (a, b) in enumerate(evs):  # a torch event creates its HIP event at its first record: here, untimed
-        a.record(streams[j % inflight])
-        b.record(streams[j % inflight])
-    # no garbage-collector pass inside the timed region: a full collection of this
-    # process's heap (torch, numpy, ctypes) stalls the host thread that issues the
-    # launches for milliseconds, longer than the 20-frame run itself
-    gc.collect()
-    gc.disable()
-    try:
+    with NoGC():
+        for j, (k, n) in enumerate(split_launches(0, nwarm, batch)):
+            issue(j, [params[(k + i) % len(params)] for i in range(n)])
+        timed = split_launches(warmup, steps, batch)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
+        for j, (a, b) in enumerate(evs):  # a torch event creates its HIP event at its first record: here, untimed
+            a.record(streams[j % inflight])
+            b.record(streams[j % inflight])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        t_each = []
         for j, (k, n) in enumerate(timed):
             issue(j, params[k:k + n], evs[j])
+            t_each.append(time.perf_counter())
         t_issued = time.perf_counter()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-    finally:
-        gc.enable()
     LAST_RUN["issue_s"] = t_issued - t0  # host time to issue the timed launches (tools/ab.py)
+    LAST_RUN["issue_each_us"] = [round((b - a) * 1e6) for a, b in zip([t0] + t_each[:-1], t_each)]
     launches = [(a.elapsed_time(b), n) for (a, b), (_, n) in zip(evs, timed)]
     jl, (kl, nl) = len(timed) - 1, timed[-1]
     return wall, launches, bufs[jl % inflight][nl - 1]
@@ -339,6 +356,14 @@ def run_distributed(scene, params, warmup, steps, a, W, H):
 
     # a p2p exchange that fails the check (IPC mapping, peer-store visibility) is
     # replaced by the RCCL gather before anything is timed
+    nogc = NoGC().__enter__()  # (collects before the verification pass; see NoGC)
+    try:
+        return _timed_distributed(make, nverify, params, warmup, steps, a, W, H, scene)
+    finally:
+        nogc.__exit__()
+
+
+def _timed_distributed(make, nverify, params, warmup, steps, a, W, H, scene):
     rs, ok, bad = make(a.exchange)
     rs.verified = {"frames": nverify, "exchange": rs.exchange, "differing": bad}
     if not ok:
@@ -352,17 +377,12 @@ def run_distributed(scene, params, warmup, steps, a, W, H):
             raise SystemExit("row-split gather: assembled frames differ from whole-frame renders")
     dist.barrier()
     torch.cuda.synchronize()
-    gc.collect()
-    gc.disable()  # as in run_single
-    try:
-        t0 = time.perf_counter()
-        rs.render(params[warmup:warmup + steps])
-        rs.host_issue_s = time.perf_counter() - t0  # host time to issue every launch and signal
-        rs.drain()
-        dist.barrier()
-        wall = time.perf_counter() - t0
-    finally:
-        gc.enable()
+    t0 = time.perf_counter()
+    rs.render(params[warmup:warmup + steps])
+    rs.host_issue_s = time.perf_counter() - t0  # host time to issue every launch and signal
+    rs.drain()
+    dist.barrier()
+    wall = time.perf_counter() - t0
     # render-launch duration of this rank's bands: the same launches (a.group frames each,
     # a.streams streams) rendered locally, HIP events on each launch's stream
     n = min(steps, 64)
@@ -644,6 +664,13 @@ def run_multi(scene, params, warmup, steps, W, H, devices, band_rows):
     dev = torch.device("cuda", devices[0])
     mr = rtamd.MultiRenderer(scene, devices, band_rows)
     try:
+        return _timed_multi(mr, params, warmup, steps, W, H, devices, dev)
+    finally:
+        mr.close()
+
+
+def _timed_multi(mr, params, warmup, steps, W, H, devices, dev):
+    with NoGC():  # (collects before the warm-up; see NoGC)
         n, exch, _ = mr.info()
         st = stream_pool(1)[0]
         nwarm = max(warmup, 16)
@@ -660,20 +687,13 @@ def run_multi(scene, params, warmup, steps, W, H, devices, band_rows):
         def sync_all():
             for d in sorted(set(devices)):
                 torch.cuda.synchronize(d)
-        gc.collect()
-        gc.disable()
-        try:
-            sync_all()
-            t0 = time.perf_counter()
-            mr.render_device_frames(params[warmup:warmup + steps], [c.data_ptr() for c, _ in ob],
-                                    [t.data_ptr() for _, t in ob], W, H, stream=st.cuda_stream)
-            sync_all()
-            wall = time.perf_counter() - t0
-        finally:
-            gc.enable()
-        return wall, ("rccl_gather" if exch == mr.RCCL else "peer_copy"), ob[-1]
-    finally:
-        mr.close()
+        sync_all()
+        t0 = time.perf_counter()
+        mr.render_device_frames(params[warmup:warmup + steps], [c.data_ptr() for c, _ in ob],
+                                [t.data_ptr() for _, t in ob], W, H, stream=st.cuda_stream)
+        sync_all()
+        wall = time.perf_counter() - t0
+    return wall, ("rccl_gather" if exch == mr.RCCL else "peer_copy"), ob[-1]
 
 
 def single_process_main(a, json_out):

@@ -77,7 +77,7 @@ def main():
                     per.append((ms, kms))
                     print(f"{name} N={n} rank {r}: {ms:.4f} ms/frame ({base / ms:.2f}x of N=1), "
                           f"{kms:.4f} ms/launch of {group}, host issue "
-                          f"{bench.LAST_RUN['issue_s'] * 1e6:.0f} us", flush=True)
+                          f"{bench.LAST_RUN['issue_s'] * 1e6:.0f} us {bench.LAST_RUN['issue_each_us']}", flush=True)
                 worst = max(ms for ms, _ in per)
                 print(f"{name} N={n}: max over ranks {worst:.4f} ms/frame -> compute-side bound "
                       f"{base / worst:.2f}x", flush=True)
