@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2401,6 +2402,14 @@ bool dropin_zero_copy() {
   return on;
 }
 
+bool dropin_trace() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_DROPIN_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // System-scope stores into host frames (kFlagHostFrame); RTAMD_HOST_STORES=agent
 // turns them off (A/B switch).
 bool host_sys_stores() {
@@ -2505,23 +2514,36 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     g_render_fault.fetch_sub(1);
     return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
   }
+  const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(s->ev0, a));
   s->stage_dirty = true;  // until its spans are cleared again below
   if (int rc = launch_render(s, fa, a)) return rc;
   HIP_TRY(hipEventRecord(s->ev1, a));
   box_out_kernel<<<(unsigned)((2 * H + 255) / 256), 256, 0, a>>>(s->d_row_span, s->h_row_span_dev, 2 * H);
   HIP_TRY(hipGetLastError());
+  const auto h1 = std::chrono::steady_clock::now();
   HIP_TRY(hipStreamSynchronize(a));
+  const auto h2 = std::chrono::steady_clock::now();
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   // the stored spans to the caller (host threads; every other pixel of the
   // caller's cleared frame already holds the staging frame's 0 / +inf), then
   // the same spans of the staging frame cleared again by the GPU, in stream
   // order before the next frame's kernel; the call does not wait for it
   rth::copy_spans(color, t, s->stage_c, s->stage_t, W, H, s->h_row_span, 0);
+  const auto h3 = std::chrono::steady_clock::now();
   drain.on = false;
   clear_spans_kernel<<<(unsigned)H, 256, 0, a>>>((uint32_t *)sc, (float *)st, s->d_row_span, W);
   HIP_TRY(hipGetLastError());
   s->stage_dirty = false;
+  if (dropin_trace()) {  // RTAMD_DROPIN_TRACE=1: host-side phases of this call (dev switch)
+    const auto h4 = std::chrono::steady_clock::now();
+    auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+    int64_t pxs = 0;
+    for (int32_t y = 0; y < H; ++y)
+      if (s->h_row_span[2 * y] <= -s->h_row_span[2 * y + 1]) pxs += -s->h_row_span[2 * y + 1] - s->h_row_span[2 * y] + 1;
+    std::fprintf(stderr, "dropin: issue %.1f, wait %.1f, copy %.1f (%lld px), clear issue %.1f us; kernel %.1f us\n",
+                 us(h0, h1), us(h1, h2), us(h2, h3), (long long)pxs, us(h3, h4), ms ? *ms * 1e3 : -1.0);
+  }
   return RT_OK;
 }
 

@@ -1023,7 +1023,12 @@ void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int
 
 void copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
                 const int32_t *span, int threads) {
-  if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), 16}));
+  static const int cap = [] {  // RTAMD_COPY_THREADS: the thread cap (A/B switch)
+    const char *e = std::getenv("RTAMD_COPY_THREADS");
+    const int v = e ? std::atoi(e) : 16;
+    return v >= 1 && v <= 64 ? v : 16;
+  }();
+  if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), cap}));
 #pragma omp parallel for schedule(static) num_threads(threads) if (threads > 1)
   for (int32_t y = 0; y < H; ++y) {
     const int32_t lo = span[2 * y], hi = -span[2 * y + 1];
