@@ -132,7 +132,8 @@ def parse():
     ap.add_argument("--exchange", choices=("p2p", "gather"), default="p2p",
                     help="N>1 frame assembly: peer stores over xGMI, or one RCCL gather per group")
     ap.add_argument("--group", type=int, default=None,
-                    help="frames per launch (at most 16; default 8 on one GPU, 16 per rank at N>1); "
+                    help="frames per launch (at most 16; default: --steps split evenly over --streams, "
+                         "at most 16); "
                          "N>1: also per completion signal / gather")
     ap.add_argument("--depth", type=int, default=3, help="N>1: groups whose slots are in flight")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the launches alternate over")
@@ -859,8 +860,14 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     a = parse()
-    if a.group is None:  # 8 whole frames per launch; a row-band rank renders 1/N of each, so 16
-        a.group = 16 if int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.gpus > 1 else 8
+    if a.group is None:
+        # the timed frames split evenly over the streams, at most 16 per launch
+        # (RT_MAX_BATCH): the driver's 20 frames go out as 10 + 10 on two streams,
+        # whose last launches then end together; 8 + 8 + 4 left the 4-frame launch
+        # alone at the end (N = 1: 0.1023 vs 0.0964 ms/frame, 3 interleaved rounds,
+        # profiles/r05/group20.txt). Longer runs take 16 per launch (whole frames
+        # level at 8-16; a row-band rank needs the 16).
+        a.group = max(1, min(16, -(-a.steps // max(1, a.streams))))
     if not 1 <= a.group <= 16:
         raise SystemExit("--group must be 1..16 (frames per launch)")
     if a.gpus < 1:
