@@ -18,7 +18,7 @@ if [ -n "$3" ]; then
   git -C $R show $3:include/rtamd.h > $S/include/rtamd.h
   SRC=$S/p/csrc/rt_device.hip
 fi
-HIPF="-std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fPIC"
+HIPF=$(make -s print-hipflags)  # the shipping build's flags (the Makefile's HIPFLAGS)
 if [ "$VAR_UNIT" = bvhgpu ]; then
   /opt/rocm/bin/hipcc $HIPF $2 -c -o build/var/rt_bvhgpu_$1.o csrc/rt_bvhgpu.hip
   DEV=build/rt_device.o BVH=build/var/rt_bvhgpu_$1.o

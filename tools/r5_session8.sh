@@ -11,4 +11,5 @@ echo "== split 20 N=8"; for r in 1 2; do for g in 10 16; do
   echo "-- $r group $g"; AB_STEPS=20 AB_GROUP=$g AB_NS=8 timeout -k 10 200 python tools/ab.py split bunny 2>&1 | grep -E "max over|N=1"
 done; done > $O/split20_group.txt; cat $O/split20_group.txt
 echo "== dist gloo"; timeout -k 10 300 env RTAMD_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 > $O/dist_gloo.log 2>&1; grep "^{" $O/dist_gloo.log | tail -1 > $O/dist_gloo.json; python -c "import json; d=json.load(open('$O/dist_gloo.json')); print(d['value'], d['n_gpus'], d['config'].get('frames_per_launch'), d.get('frame_check'))"
+echo "== variants"; bash tools/ab_oct.sh "main w6 lb2w6 oct7" 2 "bunny octree mesh_large" > $O/variants_ab.txt 2>&1; grep -v amdgpu $O/variants_ab.txt
 echo "== done"
