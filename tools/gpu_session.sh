@@ -44,7 +44,7 @@ for step in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o p -- python3 bench.py --steps 128 --warmup 16 --no-pmc --no-cpu-baseline || exit 1 ;;
     prof_driver) run prof_driver 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_driver" -o p -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc --no-cpu-baseline --detail "$OUT/prof_driver_detail.json" || exit 1
                  grep "^{" "$OUT/prof_driver.log" | tail -n 1 > "$OUT/prof_driver.json"
-                 python tools/prof_summary.py $(ls "$OUT"/prof_driver/*/p_kernel_trace.csv "$OUT"/prof_driver/p_kernel_trace.csv 2>/dev/null | head -n 1) 3 "render_persist_kernel<(anonymous namespace)::MeshS, 4, false>" 2 1 20 > "$OUT/prof_driver_phases.txt" 2>&1; cat "$OUT/prof_driver_phases.txt" ;;
+                 python tools/prof_summary.py $(ls "$OUT"/prof_driver/*/p_kernel_trace.csv "$OUT"/prof_driver/p_kernel_trace.csv 2>/dev/null | head -n 1) 2 "render_persist_kernel<(anonymous namespace)::MeshS, 4, false>" 2 1 20 > "$OUT/prof_driver_phases.txt" 2>&1; cat "$OUT/prof_driver_phases.txt" ;;
     split) run split 600 python tools/ab.py split bunny || exit 1 ;;
     split_large) run split_large 600 python tools/ab.py split mesh_large || exit 1 ;;
     benchw=*) run "bench_$arg" 600 python bench.py --workload "$arg" --steps 20 --warmup 5 --no-extra \

@@ -9,7 +9,7 @@ for roofline.one_stream the same warm-up frames on one stream (2 launches) and
 the timed one-stream launches. Dispatches are taken in Dispatch_Id order.
 usage: python tools/prof_summary.py <kernel_trace.csv> <timed launches> [kernel substring]
                                      [two-stream warm-up launches] [one-stream warm-up launches] [timed frames]
-(the driver's command, --steps 20 --warmup 5: 3 timed launches, warm-ups 2 and 1)
+(the driver's command, --steps 20 --warmup 5: 2 timed launches of 10 frames, warm-ups 2 and 1)
 With the timed frame count, the one-stream launches' summed duration per frame
 is printed too (bench.py's roofline.one_stream.kernel_ms_per_frame).
 """
