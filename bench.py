@@ -569,12 +569,20 @@ def drop_in(scene, params, W, H, frames=16):
     ms per frame including the copies, on pageable and pinned buffers, for
     three ways of calling it: `clear` (RT_FLAG_CLEAR: clear + draw fused, no
     upload, the whole frame copied back), `cleared` (RT_FLAG_CLEAR |
-    RT_FLAG_HITS_ONLY: the app's frameBuf.clear() + draw, main.cpp:197-203; no
-    upload, only the hits' bounding box copied back) and `tprev` (no flag:
-    upload of color and t, write-on-hit, the hits' box copied back)."""
+    RT_FLAG_HITS_ONLY: the app's frameBuf.clear() + draw, main.cpp:197-203; the
+    kernel stores its hits into host memory: the pinned buffers themselves, or
+    a staging frame whose stored row spans the host copies) and `tprev` (no
+    flag: upload of color and t, write-on-hit, the hits' box copied back)."""
     import numpy as np
     L = rtamd.lib()
     out = {}
+    with NoGC():  # as the timed regions: no collection lands inside one of the 16 calls
+        _drop_in_legs(scene, params, W, H, frames, L, out, np)
+    out["note"] = f"rt_render on host buffers, {W}x{H}, ms/frame incl. copies, {frames} frames each"
+    return out
+
+
+def _drop_in_legs(scene, params, W, H, frames, L, out, np):
     for pinned in (False, True):
         c = np.zeros((H, W), np.uint32)
         t = np.full((H, W), np.inf, np.float32)
@@ -601,8 +609,6 @@ def drop_in(scene, params, W, H, frames=16):
             if pinned:
                 L.rt_host_unpin(c.ctypes.data)
                 L.rt_host_unpin(t.ctypes.data)
-    out["note"] = f"rt_render on host buffers, {W}x{H}, ms/frame incl. copies, {frames} frames each"
-    return out
 
 
 def cpu_scene(src):
