@@ -1084,10 +1084,16 @@ __global__ void box_out_kernel(const int32_t *d_box, int32_t *h_box, int n) {
 }
 
 // the staging frame's stored spans (the row spans of its last frame) cleared
-// again: block y clears row y's span. A row without hits holds (INT32_MAX,
-// INT32_MAX): it returns before any index is formed from them.
-__global__ void clear_spans_kernel(uint32_t *c, float *t, const int32_t *span, int32_t W) {
+// again, and the span words reset for the next frame: block y clears row y's
+// span. A row without hits holds (INT32_MAX, INT32_MAX): it returns before
+// any index is formed from them.
+__global__ void clear_spans_kernel(uint32_t *c, float *t, int32_t *span, int32_t W) {
   const int32_t y = (int32_t)blockIdx.x, lo = span[2 * y], hi = -span[2 * y + 1];
+  __syncthreads();  // (every thread has read the row's span)
+  if (threadIdx.x == 0) {
+    span[2 * y] = INT32_MAX;
+    span[2 * y + 1] = INT32_MAX;
+  }
   if (lo > hi || lo < 0 || hi >= W) return;
   for (int32_t x = lo + (int32_t)threadIdx.x; x <= hi; x += (int32_t)blockDim.x) {
     const size_t i = (size_t)y * (size_t)W + (size_t)x;
@@ -2500,7 +2506,10 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     s->stage_dirty = true;  // (the spans of the frame in the staging frame are gone)
   }
   if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
+    // (otherwise the previous frame's clear_spans_kernel left both the staging
+    // frame and the span words reset)
     rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_row_span, 0x7FFFFFFF, (size_t)H * 2, a));
     s->stage_W = W;
     s->stage_H = H;
     s->stage_dirty = false;
@@ -2509,7 +2518,6 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   fa.t = (float *)st;
   fa.hit_box = s->d_row_span;
   fa.flags |= kFlagRowSpan;
-  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_row_span, 0x7FFFFFFF, (size_t)H * 2, a));
   if (g_render_fault.load() > 0) {
     g_render_fault.fetch_sub(1);
     return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
