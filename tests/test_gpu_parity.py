@@ -416,3 +416,22 @@ def test_group_primitives_match_scalar_forms(gpu):
         else:
             assert mt[g] == np.inf
     assert np.all(orv == 0o11111111)
+
+
+def test_fast_reciprocal_exhaustive(gpu):
+    """tri_t's reciprocal (rt_rcp.h rcp_rn: v_rcp_f32 + one fused Newton step)
+    equals the IEEE division 1 / x bit for bit for EVERY float x with
+    1e-8 <= |x| < 2^126 -- the range where the triangle test uses it (below,
+    the triangle is a miss whatever the value; above, inf and NaN take the
+    division). Exhaustive over all 2^32 bit patterns, on this GPU."""
+    import ctypes as C
+
+    from rtamd._lib import lib
+    L = lib()
+    checked, bad, first = C.c_uint64(0), C.c_uint64(0), C.c_uint32(0)
+    L.rtx_rcp_check.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    assert L.rtx_rcp_check(C.byref(checked), C.byref(bad), C.byref(first)) == 0
+    # 2 signs x 2^23 mantissas x (the 152 binades 2^-26 .. 2^125, and the part of 2^-27's binade
+    # from 1e-8 up)
+    assert 2 * 152 * (1 << 23) < checked.value < 2 * 153 * (1 << 23)
+    assert bad.value == 0, f"{bad.value} mismatches, e.g. x bits 0x{first.value:08x}"

@@ -1102,6 +1102,22 @@ __global__ void clear_spans_kernel(uint32_t *c, float *t, int32_t *span, int32_t
   }
 }
 
+// rtx_rcp_check: out[0] += floats checked, out[1] += mismatches, out[2] = bits
+// of a mismatching x
+__global__ void rcp_check_kernel(uint32_t base, unsigned long long *out) {
+  const uint32_t bits = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const float x = __uint_as_float(bits);
+  const float ax = __builtin_fabsf(x);
+  const bool in = ax >= 1e-8f && ax < 0x1p126f;
+  const bool bad = in && __float_as_uint(1.0f / x) != __float_as_uint(rtm::rcp_rn(x));
+  const unsigned long long nin = __popcll(__ballot(in)), nbad = __popcll(__ballot(bad));
+  if ((threadIdx.x & 63) == 0) {
+    if (nin) atomicAdd(out, nin);
+    if (nbad) atomicAdd(out + 1, nbad);
+  }
+  if (bad) out[2] = bits;
+}
+
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
                               float *t, int W, int H, int band_rows, int nranks) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2898,6 +2914,30 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // (band_takes_queue); < 0 restores the default threshold.
 int rtx_set_band_queue_px(int64_t px) {
   g_band_queue_px.store(px < 0 ? (int64_t)1000000 : px);
+  return RT_OK;
+}
+
+// Exhaustive check of rtm::rcp_rn (rt_rcp.h, tri_t's reciprocal) on this
+// device: every float x with 1e-8 <= |x| < 2^126 against the IEEE division
+// 1 / x. *checked = floats in that range, *bad = mismatches, *first_bad = the
+// bits of one mismatching x (0 if none). Not part of include/rtamd.h.
+int rtx_rcp_check(uint64_t *checked, uint64_t *bad, uint32_t *first_bad) {
+  if (!checked || !bad || !first_bad) return set_err(RT_E_INVALID, "NULL argument");
+  unsigned long long *d = nullptr;
+  HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
+  const uint32_t block = 256, chunk = 1u << 28;  // 2^28 bit patterns per launch
+  for (uint64_t base = 0; e == hipSuccess && base < (1ull << 32); base += chunk) {
+    rcp_check_kernel<<<chunk / block, block>>>((uint32_t)base, d);
+    e = hipGetLastError();
+  }
+  unsigned long long h[3] = {0, 0, 0};
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+  HIP_NOTE(hipFree(d));
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("rcp check: ") + hipGetErrorString(e));
+  *checked = h[0];
+  *bad = h[1];
+  *first_bad = (uint32_t)h[2];
   return RT_OK;
 }
 

@@ -9,6 +9,7 @@
 #pragma once
 #include "rt_layout.h"
 #include "rt_math.h"
+#include "rt_rcp.h"
 
 namespace rtd {
 
@@ -85,11 +86,27 @@ __device__ __forceinline__ const rtl::GNode *mesh_node(const MeshDev &sc, uint32
 // triangle_intersection (ray_pack.ispc:132-165) on one triangle already in
 // registers (v0, e1 = v1-v0, e2 = v2-v0; the subtractions are exact host-side
 // float ops, identical to the reference's). Returns t, or +inf on a miss.
+// 1: tri_t's 1 / det as rtm::rcp_rn (rt_rcp.h: the same bits for every det
+// the test uses), the division only when some lane's |det| >= 2^126, inf or
+// NaN; 0: the division always (A/B switch)
+#ifndef RT_FAST_RCP
+#define RT_FAST_RCP 1
+#endif
 __device__ __forceinline__ float tri_t(float4 a, float4 b, float4 c, f3 o, f3 d) {
   const f3 v0{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
   const f3 pvec = cross(d, e2);
   const float det = dot(e1, pvec);
-  const float inv_det = 1 / det;
+  float inv_det;
+  if constexpr (RT_FAST_RCP) {
+    // |det| < 1e-8 is a miss below whatever inv_det is
+    const bool big = !(__builtin_fabsf(det) < 0x1p126f);
+    inv_det = rtm::rcp_rn(det);
+    if (__ballot(big)) {
+      if (big) inv_det = 1 / det;
+    }
+  } else {
+    inv_det = 1 / det;
+  }
   const f3 tvec = o - v0;
   const float u = dot(tvec, pvec) * inv_det;
   const f3 qvec = cross(tvec, e1);
