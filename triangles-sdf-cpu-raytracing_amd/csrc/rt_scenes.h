@@ -99,10 +99,12 @@ __device__ __forceinline__ float tri_t(float4 a, float4 b, float4 c, f3 o, f3 d)
   float inv_det;
   if constexpr (RT_FAST_RCP) {
     // |det| < 1e-8 is a miss below whatever inv_det is
-    const bool big = !(__builtin_fabsf(det) < 0x1p126f);
     inv_det = rtm::rcp_rn(det);
-    if (__ballot(big)) {
-      if (big) inv_det = 1 / det;
+    if constexpr (RT_FAST_RCP == 1) {
+      const bool big = !(__builtin_fabsf(det) < 0x1p126f);
+      if (__ballot(big)) {
+        if (big) inv_det = 1 / det;
+      }
     }
   } else {
     inv_det = 1 / det;
