@@ -435,3 +435,34 @@ def test_fast_reciprocal_exhaustive(gpu):
     # from 1e-8 up)
     assert 2 * 152 * (1 << 23) < checked.value < 2 * 153 * (1 << 23)
     assert bad.value == 0, f"{bad.value} mismatches, e.g. x bits 0x{first.value:08x}"
+
+
+@pytest.mark.parametrize("log2_scale", [0, 60])
+def test_triangle_reciprocal_scene_bound(gpu, log2_scale):
+    """The fast reciprocal of the triangle test (tri_t<true>) is taken only by
+    rays whose direction keeps every |det| of the scene below 2^125
+    (MeshDev::dmax2); the others take the division. The bunny scaled by 2^60
+    (exact: a power of two) with rays of |d| from 1 to 2^14 puts |det| on both
+    sides of that bound (up to ~2^127); hit, t, normal and primitive id equal
+    the oracle's bit for bit, as at scale 1."""
+    import rtamd
+    from rtamd import data
+    m = rtamd.load_mesh_from_obj(data.path("stanford-bunny.obj"))
+    v = m.vPos4f.copy()
+    v[:, :3] = np.ldexp(v[:, :3], log2_scale)
+    gs = rtamd.BVHBuilder(rtamd.SimpleMesh(v, m.indices))
+    rs = cpuref.RefScene.mesh(v, m.indices)
+    o, d = _random_rays(20000, 77 + log2_scale, inside_frac=0.3)
+    o = np.ldexp(o, log2_scale).astype(np.float32)
+    rng = np.random.default_rng(5)
+    d = np.ldexp(d, rng.integers(0, 15, (len(d), 1))).astype(np.float32)
+    tn, tf = 0.0, 1e30
+    rh, rt_, rn, rp = rs.intersect_rays(o, d, tn, tf)
+    g = gs.intersect(o, d, tn, tf)
+    assert rh.sum() > 1000
+    assert np.array_equal(rh.astype(bool), g.hitten), "hit mask differs"
+    assert np.array_equal(rp, g.prim), "primitive ids differ"
+    h = g.hitten
+    assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
+    assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
+    gs.close()

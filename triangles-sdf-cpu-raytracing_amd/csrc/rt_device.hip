@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1210,6 +1211,7 @@ struct rt_scene {
   float root_box[6] = {0, 0, 0, 0, 0, 0};
   int64_t host_nodes = 0, host_inner = 0;
   uint32_t n_inner = 0;  // inner nodes on the device (MeshDev::n_inner)
+  float dmax2 = 0.0f;    // MeshDev::dmax2 (mesh_dmax2; 0: every ray takes the division)
   int32_t bvh_depth = 0;
   // grid
   float *d_vals = nullptr;
@@ -1311,7 +1313,7 @@ __global__ __launch_bounds__(256) void brick_kernel(const float *__restrict__ sr
 }
 
 MeshDev mesh_dev(const rt_scene *s) {
-  MeshDev m{s->d_nodes, s->d_tris, s->root, {}, s->coop, s->n_inner, nullptr, 0};
+  MeshDev m{s->d_nodes, s->d_tris, s->root, {}, s->coop, s->n_inner, nullptr, 0, s->dmax2};
   for (int k = 0; k < 6; ++k) m.rbox[k] = s->root_box[k];
   return m;
 }
@@ -2038,6 +2040,54 @@ int rt_bvh_export(const float *vpos4, int64_t nverts, const uint32_t *idx, int64
   return RT_OK;
 }
 
+// max over triangle slots of |e1| |e2| (float bits: the values are >= 0, so
+// their bit patterns order like them; NaN counts as +inf)
+__global__ void tri_edge_bound_kernel(const rtl::GTri *__restrict__ tris, uint32_t n, uint32_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  float m = 0.0f;
+  if (i < n) {
+    const float4 *q = reinterpret_cast<const float4 *>(tris + i);
+    const float4 b = q[1], c = q[2];
+    const float v = __builtin_sqrtf(b.x * b.x + b.y * b.y + b.z * b.z) *
+                    __builtin_sqrtf(c.x * c.x + c.y * c.y + c.z * c.z);
+    m = __builtin_isnan(v) ? kInf : v;
+  }
+  for (int off = 32; off > 0; off >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(out, __float_as_uint(m));
+}
+
+// MeshDev::dmax2 of a mesh scene: (2^124 / (2 M))^2, M = max |e1| |e2| over its
+// triangles. A ray with dot(d, d) <= dmax2 has |d| <= 2^124 / (2 M) (up to a
+// few ulps), and tri_t's float det = e1 . (d x e2) is at most sqrt(2) |e1|
+// |e2| |d| (1 + 2^-24)^5 < 1.5 M |d| <= 0.75 x 2^124 in magnitude: inside the
+// range where rtm::rcp_rn is the division. M = 0 (no triangle with both edges)
+// leaves every direction; M = inf or NaN leaves none.
+int mesh_dmax2(rt_scene *s, uint32_t n_tris) {
+  s->dmax2 = 0.0f;
+  if (n_tris == 0) return RT_OK;
+  uint32_t *d = nullptr, h = 0;
+  HIP_TRY(hipMalloc(&d, 4));
+  hipError_t e = hipMemset(d, 0, 4);
+  if (e == hipSuccess) {
+    tri_edge_bound_kernel<<<(n_tris + 255) / 256, 256>>>(s->d_tris, n_tris, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+  HIP_NOTE(hipFree(d));
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("triangle edge bound: ") + hipGetErrorString(e));
+  float M;
+  std::memcpy(&M, &h, 4);
+  if (M == 0.0f) {
+    s->dmax2 = std::numeric_limits<float>::max();
+  } else if (std::isfinite(M)) {
+    const double r = std::ldexp(1.0, 124) / (2.0 * (double)M * (1.0 + 1e-6));
+    const double r2 = r * r;
+    s->dmax2 = r2 >= (double)std::numeric_limits<float>::max() ? std::numeric_limits<float>::max()
+                                                                  : std::nextafter((float)r2, 0.0f);
+  }
+  return RT_OK;
+}
+
 int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx, int64_t nidx,
                          rt_scene **out) {
   if (!vpos4 || !idx || nverts <= 0 || nidx <= 0) return set_err(RT_E_INVALID, "empty mesh");
@@ -2061,7 +2111,8 @@ int rt_scene_create_mesh(const float *vpos4, int64_t nverts, const uint32_t *idx
     s->d_tris = static_cast<rtl::GTri *>(b.dev_tris.take());
   }
   if ((rc = upload(&s->d_nodes, b.nodes.data(), b.nodes.size(), s->dev_bytes)) ||
-      (!s->d_tris && (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes)))) {
+      (!s->d_tris && (rc = upload_padded(&s->d_tris, b.tris.data(), b.tris.size(), 8, s->dev_bytes))) ||
+      (rc = mesh_dmax2(s, b.n_tris))) {
     rt_scene_destroy(s);
     return rc;
   }
@@ -2153,6 +2204,7 @@ int rt_scene_replicate(const rt_scene *src, int device, rt_scene **out) {
   s->host_nodes = src->host_nodes;
   s->host_inner = src->host_inner;
   s->n_inner = src->n_inner;
+  s->dmax2 = src->dmax2;
   s->bvh_depth = src->bvh_depth;
   std::memcpy(s->size, src->size, sizeof s->size);
   s->grid_bricked = src->grid_bricked;

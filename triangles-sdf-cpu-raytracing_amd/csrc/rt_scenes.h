@@ -65,6 +65,11 @@ struct MeshDev {
   // [0, n_lds) are read from lnodes (a block's LDS), the rest from nodes
   const rtl::GNode *lnodes;
   uint32_t n_lds;
+  // rays with dot(d, d) <= dmax2 cannot make any triangle's |det| reach 2^125
+  // (|det| <= 1.5 |e1| |e2| |d| in float arithmetic, max |e1| |e2| of the
+  // scene measured at creation, mesh_dmax2): they take the triangle test with
+  // the fast reciprocal (tri_t<true>). 0: every ray takes the division.
+  float dmax2;
 };
 
 // Inner nodes of the top BVH levels kept in each persistent block's LDS (0:
@@ -86,26 +91,22 @@ __device__ __forceinline__ const rtl::GNode *mesh_node(const MeshDev &sc, uint32
 // triangle_intersection (ray_pack.ispc:132-165) on one triangle already in
 // registers (v0, e1 = v1-v0, e2 = v2-v0; the subtractions are exact host-side
 // float ops, identical to the reference's). Returns t, or +inf on a miss.
-// 1: tri_t's 1 / det as rtm::rcp_rn (rt_rcp.h: the same bits for every det
-// the test uses), the division only when some lane's |det| >= 2^126, inf or
-// NaN; 0: the division always (A/B switch)
+// FR (fast reciprocal): 1 / det as rtm::rcp_rn (rt_rcp.h), the same bits as
+// the division for every 1e-8 <= |det| < 2^126; taken by rays whose direction
+// keeps every |det| of the scene below 2^125 (MeshDev::dmax2; |det| < 1e-8 is
+// a miss below whatever inv_det is). RT_FAST_RCP=0: the division always (A/B
+// switch).
 #ifndef RT_FAST_RCP
 #define RT_FAST_RCP 1
 #endif
+template <bool FR>
 __device__ __forceinline__ float tri_t(float4 a, float4 b, float4 c, f3 o, f3 d) {
   const f3 v0{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
   const f3 pvec = cross(d, e2);
   const float det = dot(e1, pvec);
   float inv_det;
-  if constexpr (RT_FAST_RCP) {
-    // |det| < 1e-8 is a miss below whatever inv_det is
+  if constexpr (FR && RT_FAST_RCP) {
     inv_det = rtm::rcp_rn(det);
-    if constexpr (RT_FAST_RCP == 1) {
-      const bool big = !(__builtin_fabsf(det) < 0x1p126f);
-      if (__ballot(big)) {
-        if (big) inv_det = 1 / det;
-      }
-    }
   } else {
     inv_det = 1 / det;
   }
@@ -139,7 +140,7 @@ __device__ __forceinline__ f3 tri_normal(const rtl::GTri *__restrict__ tris, uin
 #ifndef RT_LEAF_BATCH_PRIMARY
 #define RT_LEAF_BATCH_PRIMARY 4
 #endif
-template <uint32_t B = RT_LEAF_BATCH, class CT>
+template <uint32_t B = RT_LEAF_BATCH, bool FR = false, class CT>
 __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, uint32_t w, f3 o,
                                           f3 d, float &lt, uint32_t &lk, CT &cnt) {
   const uint32_t first = (w >> 3) & rtl::kMaxLeafFirstTri;
@@ -157,7 +158,7 @@ __device__ __forceinline__ void leaf_test(const rtl::GTri *__restrict__ tris, ui
     }
     float tk[B];
 #pragma unroll
-    for (uint32_t k = 0; k < B; ++k) tk[k] = tri_t(a[k], b[k], c[k], o, d);
+    for (uint32_t k = 0; k < B; ++k) tk[k] = tri_t<FR>(a[k], b[k], c[k], o, d);
 #pragma unroll
     for (uint32_t k = 0; k < B; ++k)
       if (base + k < n && lt > tk[k]) { lt = tk[k]; lk = first + base + k; }
@@ -346,7 +347,7 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       if (word & rtl::kLeafBit) {
         float lt = kInf;
         uint32_t lk = rtl::kInvalidChild;
-        leaf_test<LB>(sc.tris, word, o, d, lt, lk, cnt);
+        leaf_test<LB, FAST>(sc.tris, word, o, d, lt, lk, cnt);
         if (lk != rtl::kInvalidChild) {
           if (ANY) { gbest = lt; gk = lk; break; }
           if (lt < fbest) fbest = lt;
@@ -537,7 +538,7 @@ __device__ __forceinline__ void mesh_run_coop(const MeshDev &sc, f3 o, f3 d, f3 
         float tk = kInf;
         if ((uint32_t)k < n) {
           const float4 *q = reinterpret_cast<const float4 *>(sc.tris + first + k);
-          tk = tri_t(q[0], q[1], q[2], o, d);
+          tk = tri_t<FAST>(q[0], q[1], q[2], o, d);
           if (!(tk < kInf)) tk = kInf;  // a NaN t never wins the strict scan
         }
         uint32_t kk = (uint32_t)k;
@@ -627,7 +628,9 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   const int lane = threadIdx.x & 63;
   LdsStack<BLOCK> st{stk_block + threadIdx.x};
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
-  const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+  // fast: the finite-1/d slab forms and the fast reciprocal (MeshDev::dmax2)
+  const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z) &&
+                    dot(d, d) <= sc.dmax2;
   MState S{rtl::kInvalidChild, 0u, 0u, sc.root, rtl::kInvalidChild, rtl::kInvalidChild, kInf, 0.0f, kInf, 0,
            false};
   bool pending = false;
@@ -719,7 +722,8 @@ __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float 
                                      rtl::kInvalidChild, false, 0, out_t, out_k, cnt);
   uint32_t l, c, cwf;
   float tf;
-  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z)) {
+  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z) &&
+      dot(d, d) <= sc.dmax2) {  // (see mesh_primary_wave)
     if (!mesh_root<true>(sc, o, inv, tNear, tFar, l, c, tf, cwf, cnt)) return false;
     return mesh_continue<BLOCK, ANY, true>(sc, o, d, inv, tNear, tFar, st, rtl::kInvalidChild, l, c, tf,
                                            cwf, true, 1, out_t, out_k, cnt);
