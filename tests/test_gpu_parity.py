@@ -469,23 +469,3 @@ def test_triangle_reciprocal_scene_bound(gpu, log2_scale):
     assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
     assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
     gs.close()
-
-
-@pytest.mark.parametrize("mode,n", [(0, 0), (1, 1 << 32), (2, 1 << 32), (3, 0)])
-def test_fast_division(gpu, mode, n):
-    """The ray setup's divisions (rt_rcp.h: div_rn for the eye ray, rcp_any for
-    1 / d) give the IEEE division's bits: (0) the eye ray's 2 (x + 1/2) / W for
-    EVERY x < W <= 32768; (1) 2^32 pairs of random bit patterns (guards,
-    zeros, infinities, NaN, subnormals, the division branch); (2) 2^32 pairs of
-    normal floats with exponents in [-40, 40] (the fused correction itself);
-    (3) rcp_any over all 2^32 bit patterns."""
-    import ctypes as C
-
-    from rtamd._lib import lib
-    L = lib()
-    out = (C.c_uint64 * 3)()
-    L.rtx_div_check.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
-    assert L.rtx_div_check(mode, n, 12345, out) == 0
-    expect = {0: 32768 * 32769 // 2, 1: n, 2: n, 3: 1 << 32}[mode]
-    assert out[0] == expect
-    assert out[1] == 0, f"{out[1]} mismatches, e.g. a, b bits 0x{out[2] & 0xFFFFFFFF:08x}, 0x{out[2] >> 32:08x}"

@@ -1119,62 +1119,6 @@ __global__ void rcp_check_kernel(uint32_t base, unsigned long long *out) {
   if (bad) out[2] = bits;
 }
 
-// rtx_div_check: rtm::div_rn / rtm::rcp_any against the division.
-// mode 0: 2 (x + 1/2) / W for every W in [1, 32768] and x < W (blockIdx.y = W - 1);
-// mode 1: n pairs of random bit patterns; mode 2: n pairs of random normal
-// floats with exponents in [-40, 40] (the correction's own range); mode 3:
-// rcp_any over all 2^32 patterns (base + index). out[0] += checked, out[1] +=
-// mismatches, out[2] = a mismatching a's bits | b's bits << 32
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-__global__ void div_check_kernel(int mode, uint64_t base, uint64_t seed, unsigned long long *out) {
-  uint64_t n_in = 0, n_bad = 0, bad_ab = 0;
-  if (mode == 0) {
-    const int W = (int)blockIdx.y + 1;
-    for (int x = (int)threadIdx.x; x < W; x += (int)blockDim.x) {
-      const float a = 2.0f * ((float)x + 0.5f), b = (float)W;
-      ++n_in;
-      if (__float_as_uint(rtm::div_rn(a, b)) != __float_as_uint(a / b)) {
-        ++n_bad;
-        bad_ab = __float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
-      }
-    }
-  } else {
-    const uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (mode == 3) {
-      const float x = __uint_as_float((uint32_t)i);
-      n_in = 1;
-      if (__float_as_uint(rtm::rcp_any(x)) != __float_as_uint(1.0f / x)) {
-        n_bad = 1;
-        bad_ab = (uint32_t)i;
-      }
-    } else {
-      const uint64_t h = mix64(i ^ (seed << 40));
-      uint32_t ua = (uint32_t)h, ub = (uint32_t)(h >> 32);
-      if (mode == 2) {  // sign | exponent in [-40, 40] | random mantissa
-        const uint64_t g = mix64(h);
-        ua = (ua & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)(g % 81)) << 23);
-        ub = (ub & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)((g >> 8) % 81)) << 23);
-      }
-      const float a = __uint_as_float(ua), b = __uint_as_float(ub);
-      n_in = 1;
-      if (__float_as_uint(rtm::div_rn(a, b)) != __float_as_uint(a / b)) {
-        n_bad = 1;
-        bad_ab = ua | ((uint64_t)ub << 32);
-      }
-    }
-  }
-  if (n_in) atomicAdd(out, (unsigned long long)n_in);
-  if (n_bad) {
-    atomicAdd(out + 1, (unsigned long long)n_bad);
-    out[2] = bad_ab;
-  }
-}
-
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
                               float *t, int W, int H, int band_rows, int nranks) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3046,35 +2990,6 @@ int rtx_rcp_check(uint64_t *checked, uint64_t *bad, uint32_t *first_bad) {
   *checked = h[0];
   *bad = h[1];
   *first_bad = (uint32_t)h[2];
-  return RT_OK;
-}
-
-// The checks behind rt_rcp.h's div_rn / rcp_any on this device (see
-// div_check_kernel for the modes; n: pairs for the random modes). out[0] =
-// checked, out[1] = mismatches, out[2] = one mismatching pair's bits. Not
-// part of include/rtamd.h.
-int rtx_div_check(int32_t mode, uint64_t n, uint64_t seed, uint64_t out[3]) {
-  if (!out || mode < 0 || mode > 3) return set_err(RT_E_INVALID, "bad arguments");
-  unsigned long long *d = nullptr;
-  HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));
-  hipError_t e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
-  const uint32_t block = 256;
-  if (e == hipSuccess && mode == 0) {
-    div_check_kernel<<<dim3(1, 32768), block>>>(0, 0, seed, d);
-    e = hipGetLastError();
-  } else if (e == hipSuccess) {
-    const uint64_t total = mode == 3 ? (1ull << 32) : n, chunk = 1ull << 28;
-    for (uint64_t b0 = 0; e == hipSuccess && b0 < total; b0 += chunk) {
-      const uint64_t m = std::min(chunk, total - b0);
-      div_check_kernel<<<(unsigned)((m + block - 1) / block), block>>>(mode, b0, seed, d);
-      e = hipGetLastError();
-    }
-  }
-  unsigned long long h[3] = {0, 0, 0};
-  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
-  HIP_NOTE(hipFree(d));
-  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("div check: ") + hipGetErrorString(e));
-  for (int i = 0; i < 3; ++i) out[i] = h[i];
   return RT_OK;
 }
 

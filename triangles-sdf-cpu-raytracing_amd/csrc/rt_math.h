@@ -14,8 +14,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "rt_rcp.h"
-
 namespace rtd {
 
 struct f3 {
@@ -180,34 +178,14 @@ __device__ __forceinline__ f4 mat_mul(const float *m, f4 v) {
 // Renderer::draw ray generation (raytracing.cpp:83-88) with LiteMath
 // EyeRayDir4f restated: pos=(2x/w-1, 2y/h-1, 0, 1); pos=P*pos;
 // pos/=pos.w; dir=normalize(pos.xyz); world dir = (viewInv*(dir,0)).xyz.
-// 1: the eye ray's divisions and the ray's 1 / d as rtm::div_rn / rtm::rcp_any
-// (rt_rcp.h: the division's bits, checked), 0: the divisions (A/B switch)
-#ifndef RT_FAST_DIV
-#define RT_FAST_DIV 1
-#endif
-__device__ __forceinline__ float div_x(float a, float b) {
-#if RT_FAST_DIV
-  return rtm::div_rn(a, b);
-#else
-  return a / b;
-#endif
-}
-__device__ __forceinline__ float rcp_x(float b) {
-#if RT_FAST_DIV
-  return rtm::rcp_any(b);
-#else
-  return 1.0f / b;
-#endif
-}
 __device__ __forceinline__ f3 eye_ray(int x, int y, int W, int H, const float *projInv,
                                       const float *viewInv) {
   const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
-  f4 pos{div_x(2.0f * fx, (float)W) - 1.0f, div_x(2.0f * fy, (float)H) - 1.0f, 0.0f, 1.0f};
+  f4 pos{2.0f * fx / (float)W - 1.0f, 2.0f * fy / (float)H - 1.0f, 0.0f, 1.0f};
   pos = mat_mul(projInv, pos);
   const float w = pos.w;
-  pos = f4{div_x(pos.x, w), div_x(pos.y, w), div_x(pos.z, w), pos.w / w};
-  const float l = len(f3{pos.x, pos.y, pos.z});
-  const f3 d{div_x(pos.x, l), div_x(pos.y, l), div_x(pos.z, l)};
+  pos = f4{pos.x / w, pos.y / w, pos.z / w, pos.w / w};
+  const f3 d = normalize(f3{pos.x, pos.y, pos.z});
   const f4 r = mat_mul(viewInv, f4{d.x, d.y, d.z, 0.0f});
   return f3{r.x, r.y, r.z};
 }

@@ -627,7 +627,7 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   NoCnt cnt;
   const int lane = threadIdx.x & 63;
   LdsStack<BLOCK> st{stk_block + threadIdx.x};
-  const f3 inv{rcp_x(d.x), rcp_x(d.y), rcp_x(d.z)};  // 1.0f / rayDir (:273)
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
   // fast: the finite-1/d slab forms and the fast reciprocal (MeshDev::dmax2)
   const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z) &&
                     dot(d, d) <= sc.dmax2;
@@ -715,7 +715,7 @@ template <int BLOCK, bool ANY, class CT>
 __device__ __forceinline__ bool mesh_trace(const MeshDev &sc, f3 o, f3 d, float tNear, float tFar,
                                            LdsStack<BLOCK> st, float &out_t, uint32_t &out_k,
                                            CT &cnt) {
-  const f3 inv{rcp_x(d.x), rcp_x(d.y), rcp_x(d.z)};  // 1.0f / rayDir (:273)
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // 1.0f / rayDir (:273)
   if (sc.root == rtl::kInvalidChild) return false;
   if (sc.root & rtl::kLeafBit)
     return mesh_continue<BLOCK, ANY>(sc, o, d, inv, tNear, tFar, st, sc.root, 0u, 0u, 0.0f,
@@ -935,7 +935,7 @@ enum { RAY_PENDING = 0, RAY_MISS = 1, RAY_HIT = 2 };
 template <int kMode, class CT>
 __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float tNear, float tFar,
                                            float &out_t, f3 &hp, uint32_t &cell, CT &cnt) {
-  const f3 inv{rcp_x(d.x), rcp_x(d.y), rcp_x(d.z)};
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   float t1, t2;
   bbox_intersection(f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
@@ -1514,7 +1514,7 @@ template <int BLOCK, bool NEED_NORMAL, bool PACK, class CT>
 __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tNear, float tFar,
                                           LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                           uint32_t &out_node, CT &cnt) {
-  const f3 inv{rcp_x(d.x), rcp_x(d.y), rcp_x(d.z)};
+  const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z))
     return oct_trace_t<BLOCK, NEED_NORMAL, true, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
   return oct_trace_t<BLOCK, NEED_NORMAL, false, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
