@@ -469,3 +469,52 @@ def test_triangle_reciprocal_scene_bound(gpu, log2_scale):
     assert np.array_equal(rt_[h].view(np.uint32), g.t[h].view(np.uint32)), "t differs"
     assert np.array_equal(rn[h].view(np.uint32), g.normal[h].view(np.uint32)), "normal differs"
     gs.close()
+
+
+@pytest.mark.parametrize("mode,n", [(0, 0), (1, 1 << 32)])
+def test_fast_eye_division(gpu, mode, n):
+    """eye_ray_fast's divisions (rt_rcp.h div_mk: the checked reciprocal and one
+    fused correction) give the IEEE division's bits: (0) 2 (x + 1/2) / W for
+    EVERY x < W <= 32768; (1) 2^32 random pairs over the ranges fast_eye_ok
+    guarantees (|a| in [2^-72, 2^24] or +-0, |b| in [2^-20, 2^24])."""
+    import ctypes as C
+
+    from rtamd._lib import lib
+    L = lib()
+    out = (C.c_uint64 * 3)()
+    L.rtx_div_check.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
+    assert L.rtx_div_check(mode, n, 2024, out) == 0
+    assert out[0] == (32768 * 32769 // 2 if mode == 0 else n)
+    assert out[1] == 0, f"{out[1]} mismatches, e.g. a, b bits 0x{out[2] & 0xFFFFFFFF:08x}, 0x{out[2] >> 32:08x}"
+
+
+@pytest.mark.parametrize("variant", ["reference", "offcenter", "scaled"])
+def test_eye_ray_projections(gpu, variant):
+    """Frames equal the oracle's bit for bit whichever eye-ray path the
+    projection selects: the reference's perspective and an off-centre one take
+    eye_ray_fast (fast_eye_ok), the same perspective scaled by 2^12 (the same
+    rays, entries out of its range) takes the divisions."""
+    import ctypes as C
+
+    import rtamd
+    name, W, H = "stanford-bunny.obj", 320, 180
+    sm, plane, sh, rf = S.MODES["default"]
+    pos = (0.3, 0.2, 2.4)
+    vi, pi = cpuref.camera_matrices(pos, (0, 0, 0), (0, 1, 0), 45.0, W / H, 0.01, 100.0)
+    pi = np.array(pi, np.float32).reshape(-1).copy()
+    if variant == "offcenter":
+        pi[12] += np.float32(0.25)
+        pi[13] -= np.float32(0.125)
+    elif variant == "scaled":
+        pi *= np.float32(2.0 ** 12)
+    L = rtamd.lib()
+    L.rtx_fast_eye_ok.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+    assert L.rtx_fast_eye_ok(pi.ctypes.data, W, H) == (0 if variant == "scaled" else 1)
+    rs, gs = S.ref_scene(name), S.gpu_scene(name)
+    S.set_planes(name, "default", rs, gs)
+    rc, rt_, _, _ = rs.render(cpuref.make_params(pos, vi, pi, (2, 2, 2), sm, sh, rf), W, H)
+    c = np.zeros((H, W), np.uint32)
+    t = np.full((H, W), np.inf, np.float32)
+    gs.render(rtamd.render_params(pos, vi, pi, (2, 2, 2), sm, sh, rf), c, t, clear=True)
+    assert np.array_equal(c, rc), int((c != rc).sum())
+    assert np.array_equal(t.view(np.uint32), rt_.view(np.uint32))

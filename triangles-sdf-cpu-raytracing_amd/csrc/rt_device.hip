@@ -348,6 +348,9 @@ constexpr uint32_t kSysStoreFlags = RT_FLAG_TILE_NATURAL;
 constexpr uint32_t kFlagHostFrame = 1u << 30;
 // Internal flag: FrameArgs::hit_box holds per-row spans (see FrameArgs).
 constexpr uint32_t kFlagRowSpan = 1u << 29;
+// Internal flag: the frame's eye rays take eye_ray_fast (fill_frame sets it
+// when fast_eye_ok holds for its projection and size).
+constexpr uint32_t kFlagFastEye = 1u << 28;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
   if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -409,7 +412,11 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     const int yo = image_row(active ? yl : 0, fa);
     const int y = fa.H - yo - 1;  // loop row y is stored to image row H-y-1 (raytracing.cpp:82)
     const f3 o{fa.P.camera_pos[0], fa.P.camera_pos[1], fa.P.camera_pos[2]};
-    const f3 d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+    f3 d;
+    if (fa.flags & kFlagFastEye)
+      d = eye_ray_fast(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
+    else
+      d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
     // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
     // full frame's own row (a peer's frame mapped over xGMI)
     const bool peer = (fa.flags & kSysStoreFlags) != 0;
@@ -1117,6 +1124,50 @@ __global__ void rcp_check_kernel(uint32_t base, unsigned long long *out) {
     if (nbad) atomicAdd(out + 1, nbad);
   }
   if (bad) out[2] = bits;
+}
+
+// rtx_div_check: rtm::div_mk against the division. mode 0: 2 (x + 1/2) / W for
+// every W in [1, 32768] and x < W (blockIdx.y = W - 1); mode 1: random pairs in
+// the eye ray's ranges (|a| in [2^-72, 2^24] or +-0, |b| in [2^-20, 2^24],
+// random signs and mantissas). out[0] += checked, out[1] += mismatches,
+// out[2] = a mismatching pair (a's bits | b's bits << 32)
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void div_check_kernel(int mode, uint64_t base, uint64_t seed, unsigned long long *out) {
+  uint64_t n_in = 0, n_bad = 0, bad_ab = 0;
+  if (mode == 0) {
+    const int W = (int)blockIdx.y + 1;
+    for (int x = (int)threadIdx.x; x < W; x += (int)blockDim.x) {
+      const float a = 2.0f * ((float)x + 0.5f), b = (float)W;
+      ++n_in;
+      if (__float_as_uint(rtm::div_mk(a, b)) != __float_as_uint(a / b)) {
+        ++n_bad;
+        bad_ab = __float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
+      }
+    }
+  } else {
+    const uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t h = mix64(i ^ (seed << 40)), g = mix64(h);
+    const uint32_t ea = 127 - 72 + (uint32_t)(g % 97), eb = 127 - 20 + (uint32_t)((g >> 16) % 45);
+    uint32_t ua = ((uint32_t)h & 0x807FFFFFu) | (ea << 23);
+    const uint32_t ub = ((uint32_t)(h >> 32) & 0x807FFFFFu) | (eb << 23);
+    if (((g >> 32) & 63) == 0) ua &= 0x80000000u;  // +-0 numerators
+    const float a = __uint_as_float(ua), b = __uint_as_float(ub);
+    n_in = 1;
+    if (__float_as_uint(rtm::div_mk(a, b)) != __float_as_uint(a / b)) {
+      n_bad = 1;
+      bad_ab = ua | ((uint64_t)ub << 32);
+    }
+  }
+  if (n_in) atomicAdd(out, (unsigned long long)n_in);
+  if (n_bad) {
+    atomicAdd(out + 1, (unsigned long long)n_bad);
+    out[2] = bad_ab;
+  }
 }
 
 __global__ void untile_kernel(const uint32_t *pc, const float *pt, int64_t per_rank, uint32_t *c,
@@ -1836,6 +1887,43 @@ int check_params(const rt_render_params *p, int32_t W, int32_t H) {
   return RT_OK;
 }
 
+// Whether eye_ray_fast gives eye_ray's bits for every pixel of a W x H frame
+// with this inverse projection: the operand ranges rtm::div_mk needs, bounded
+// over the whole frame. Every entry zero or of magnitude in [2^-10, 2^10] (the
+// z column, which meets z = 0, only finite), so a
+// nonzero pos component (NDC steps >= 2^-24) is at least ~2^-60 and at most
+// 3 x 2^10; |w| >= 2^-10 over [-1, 1]^2 (one sign); a component of pos whose
+// constant term dominates keeps |p| >= 2^-20. Then pos / w, p and p / |p|
+// stay in [2^-96, 2^44] (or are +-0). 2 fx / W: every W <= 32768 is checked.
+// The reference's projection (perspectiveMatrix(45, W/H, 0.01, 100)) passes.
+// RTAMD_FAST_EYE=0 keeps the divisions (A/B switch)
+bool fast_eye_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_FAST_EYE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool fast_eye_ok(const float *m, int32_t W, int32_t H) {
+  if (W > 32768 || H > 32768) return false;
+  for (int i = 0; i < 16; ++i) {
+    const float a = std::fabs(m[i]);
+    if (i >= 8 && i < 12) {  // the z column meets z = 0: any finite entry adds +-0
+      if (!std::isfinite(m[i])) return false;
+    } else if (!(m[i] == 0.0f || (a >= 0x1p-10f && a <= 0x1p10f))) {
+      return false;
+    }
+  }
+  const double wc = std::fabs((double)m[15]), wr = std::fabs((double)m[3]) + std::fabs((double)m[7]);
+  if (!(wc - wr >= 0x1p-10)) return false;
+  const double wmax = wc + wr;
+  double lmin = 0.0;
+  for (int i = 0; i < 3; ++i)
+    lmin = std::max(lmin, (std::fabs((double)m[12 + i]) - std::fabs((double)m[i]) - std::fabs((double)m[4 + i])) / wmax);
+  return lmin >= 0x1p-20;
+}
+
 int fill_frame(FrameArgs &fa, const rt_render_params *p, uint32_t *c, float *t, int32_t W, int32_t H,
                uint32_t flags, const rt_tile *tile) {
   fa.P = *p;
@@ -1863,6 +1951,7 @@ int fill_frame(FrameArgs &fa, const rt_render_params *p, uint32_t *c, float *t, 
     fa.nranks = tile->num_ranks;
     fa.rows_local = (int32_t)(rt_tile_pixels(W, H, tile) / W);
   }
+  if (fast_eye_enabled() && fast_eye_ok(p->proj_inv, W, H)) fa.flags |= kFlagFastEye;
   return RT_OK;
 }
 
@@ -2990,6 +3079,40 @@ int rtx_rcp_check(uint64_t *checked, uint64_t *bad, uint32_t *first_bad) {
   *checked = h[0];
   *bad = h[1];
   *first_bad = (uint32_t)h[2];
+  return RT_OK;
+}
+
+// fast_eye_ok for tests (host only): 1 when a W x H frame with this inverse
+// projection takes eye_ray_fast. Not part of include/rtamd.h.
+int rtx_fast_eye_ok(const float *proj_inv, int32_t W, int32_t H) {
+  return proj_inv && fast_eye_ok(proj_inv, W, H) ? 1 : 0;
+}
+
+// The checks behind rtm::div_mk on this device (div_check_kernel's modes; n:
+// pairs for mode 1). out[0] = checked, out[1] = mismatches, out[2] = one
+// mismatching pair's bits. Not part of include/rtamd.h.
+int rtx_div_check(int32_t mode, uint64_t n, uint64_t seed, uint64_t out[3]) {
+  if (!out || mode < 0 || mode > 1) return set_err(RT_E_INVALID, "bad arguments");
+  unsigned long long *d = nullptr;
+  HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
+  const uint32_t block = 256;
+  if (e == hipSuccess && mode == 0) {
+    div_check_kernel<<<dim3(1, 32768), block>>>(0, 0, seed, d);
+    e = hipGetLastError();
+  } else if (e == hipSuccess) {
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t b0 = 0; e == hipSuccess && b0 < n; b0 += chunk) {
+      const uint64_t m = std::min(chunk, n - b0);
+      div_check_kernel<<<(unsigned)((m + block - 1) / block), block>>>(mode, b0, seed, d);
+      e = hipGetLastError();
+    }
+  }
+  unsigned long long h[3] = {0, 0, 0};
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+  HIP_NOTE(hipFree(d));
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("div check: ") + hipGetErrorString(e));
+  for (int i = 0; i < 3; ++i) out[i] = h[i];
   return RT_OK;
 }
 

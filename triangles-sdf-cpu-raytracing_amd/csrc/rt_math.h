@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_rcp.h"
+
 namespace rtd {
 
 struct f3 {
@@ -186,6 +188,22 @@ __device__ __forceinline__ f3 eye_ray(int x, int y, int W, int H, const float *p
   const float w = pos.w;
   pos = f4{pos.x / w, pos.y / w, pos.z / w, pos.w / w};
   const f3 d = normalize(f3{pos.x, pos.y, pos.z});
+  const f4 r = mat_mul(viewInv, f4{d.x, d.y, d.z, 0.0f});
+  return f3{r.x, r.y, r.z};
+}
+
+// eye_ray with its divisions as rtm::div_mk (the same bits), for frames whose
+// projection keeps every operand in div_mk's range (fast_eye_ok on the host,
+// kFlagFastEye): 2 fx / W and 2 fy / H (W, H <= 32768), pos / w and p / |p|.
+__device__ __forceinline__ f3 eye_ray_fast(int x, int y, int W, int H, const float *projInv,
+                                           const float *viewInv) {
+  const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+  f4 pos{rtm::div_mk(2.0f * fx, (float)W) - 1.0f, rtm::div_mk(2.0f * fy, (float)H) - 1.0f, 0.0f, 1.0f};
+  pos = mat_mul(projInv, pos);
+  const float w = pos.w;
+  const f3 p{rtm::div_mk(pos.x, w), rtm::div_mk(pos.y, w), rtm::div_mk(pos.z, w)};
+  const float l = len(p);
+  const f3 d{rtm::div_mk(p.x, l), rtm::div_mk(p.y, l), rtm::div_mk(p.z, l)};
   const f4 r = mat_mul(viewInv, f4{d.x, d.y, d.z, 0.0f});
   return f3{r.x, r.y, r.z};
 }

@@ -18,4 +18,20 @@ __device__ __forceinline__ float rcp_rn(float x) {
   return __builtin_fmaf(r, e, r);
 }
 
+// a / b correctly rounded for operands in the ranges the caller guarantees:
+// y = rcp_rn(b) (b in its checked range), q = a y, the remainder a - b q
+// exact by one fma, then the correction q + rem y (Markstein), which rounds
+// to the quotient when a, q and the remainder stay normal: here
+// |a| in [2^-102, 2^100] or a = +-0 (whose q = a y already carries the
+// quotient's sign), |q| in [2^-100, 2^100]. Checked on the GPU: every
+// 2 (x + 1/2) / W with x < W <= 32768 and 2^32 random pairs in the eye ray's
+// ranges (rtx_div_check, tests/test_gpu_parity.py::test_fast_eye_division).
+__device__ __forceinline__ float div_mk(float a, float b) {
+  const float y = rcp_rn(b);
+  const float q = a * y;
+  const float rem = __builtin_fmaf(-b, q, a);
+  const float q1 = __builtin_fmaf(rem, y, q);
+  return a == 0.0f ? q : q1;
+}
+
 }  // namespace rtm
