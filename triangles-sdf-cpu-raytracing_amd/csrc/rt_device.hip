@@ -1436,13 +1436,12 @@ void launch_render_t(const S &sc, const PlaneDev &pl, const FrameArgs &fa, bool 
   }
 }
 
-// The pageable drop-in path's staging frame (render_cleared_zero_copy) back
-// to the heap; the caller has synchronised the streams that use it.
+// The pageable drop-in path's staging frame (render_cleared_zero_copy) freed;
+// the caller has synchronised the streams that use it.
 void stage_free(rt_scene *s) {
   for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
     if (*q) {
-      HIP_NOTE(hipHostUnregister(*q));
-      std::free(*q);
+      HIP_NOTE(hipHostFree(*q));
       *q = nullptr;
     }
   }
@@ -2628,17 +2627,12 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   if (px > s->stage_cap) {
     HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
     stage_free(s);
-    // page-aligned host memory registered with the runtime, mapped (as
-    // rt_host_pin does for the caller's buffers)
-    const size_t bytes = (px * 4 + 4095) & ~(size_t)4095;
+    // pinned, mapped host memory the runtime owns: never handed back to the
+    // process heap, so no caller buffer can later land on pages this library
+    // registered and unregistered (aligned_alloc + hipHostRegister did that;
+    // see DESIGN.md section 0d, the GPU-suite stop of round 5)
     for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
-      *q = std::aligned_alloc(4096, bytes);
-      if (!*q) {
-        stage_free(s);
-        return set_err(RT_E_DEVICE, "staging frame: out of host memory");
-      }
-      if (const hipError_t e = hipHostRegister(*q, bytes, hipHostRegisterMapped)) {
-        std::free(*q);
+      if (const hipError_t e = hipHostMalloc(q, px * 4, hipHostMallocDefault)) {
         *q = nullptr;
         stage_free(s);
         return set_err(RT_E_DEVICE, std::string("staging frame: ") + hipGetErrorString(e));
