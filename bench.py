@@ -540,6 +540,7 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
     scene.set_plane(rtamd.Plane((0.0, 1.0, 0.0), off) if mode == "default" else None)
     prm = orbit_params(warmup + steps, W, H, mode)
     wall, launches, (lc, lt) = run_single(scene, prm, warmup, steps, W, H, inflight=streams, batch=group)
+    issue_us = list(LAST_RUN["issue_each_us"])
     ms_step = wall * 1e3 / steps
     _, _, (c1, t1) = run_single(scene, prm[warmup + steps - 1:], 0, 1, W, H, inflight=1)  # as the headline's check
     frame_ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
@@ -558,7 +559,8 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
         out["traced_rays_per_px"] = rays
         out["traced_value"] = round(W * H * rays * steps / wall / 1e6, 1)
     detail[key] = {"workload": desc, "roofline": rl, "one_stream": one, "work_per_ray": per_ray,
-                   "launch_ms": [round(ms, 5) for ms, _ in launches], "pmc_per_launch": pmc.get(key)}
+                   "launch_ms": [round(ms, 5) for ms, _ in launches], "issue_us": issue_us,
+                   "wall_ms": round(wall * 1e3, 4), "pmc_per_launch": pmc.get(key)}
     scene.close()
     torch.cuda.synchronize()
     return out
@@ -927,6 +929,7 @@ def main():
         wall, launches, (lc, lt) = run_single(scene, params, a.warmup, a.steps, W, H, inflight=a.streams,
                                               batch=a.group)
         detail["headline_launch_ms"] = [round(ms, 5) for ms, _ in launches]
+        detail["headline_issue_us"] = list(LAST_RUN["issue_each_us"])
         # the last timed frame (the persistent multi-frame kernel) must equal the
         # same frame rendered alone by the one-frame kernel (render_kernel): both
         # are bit-exact against the oracle in tests/, so a timed path that drops
