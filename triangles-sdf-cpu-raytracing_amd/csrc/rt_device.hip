@@ -2588,11 +2588,11 @@ bool host_sys_stores() {
 // those -- into HOST memory (zero-copy), so no download follows the kernel:
 //  * buffers pinned by rt_host_pin: the hits go straight into them;
 //  * pageable buffers: into the scene's pinned staging frame, which is kept
-//    cleared. The frame renders as dropin_bands() contiguous row bands, one
-//    launch each on one stream, each recording its hits' bounding box; as
-//    each band ends, the host copies its box to the caller's buffers (OpenMP
-//    rows) while the next band renders, and at the end the GPU clears the
-//    boxes in the staging frame again, in stream order before the next frame.
+//    cleared. The kernel records, per row, the span of the pixels it stored
+//    (kFlagRowSpan); box_out_kernel moves the spans to mapped host memory, the
+//    host copies just those spans to the caller's buffers (OpenMP rows), and
+//    the GPU clears the same spans of the staging frame again
+//    (clear_spans_kernel), in stream order before the next frame.
 int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *t, int32_t W, int32_t H,
                              float *ms) {
   const size_t px = (size_t)W * H;
@@ -3049,6 +3049,16 @@ int rtx_grp_test(const float *keys, int32_t n, float *st, uint32_t *sid, float *
 // (band_takes_queue); < 0 restores the default threshold.
 int rtx_set_band_queue_px(int64_t px) {
   g_band_queue_px.store(px < 0 ? (int64_t)1000000 : px);
+  return RT_OK;
+}
+
+// The pageable drop-in's host copy (rth::copy_spans) on caller arrays, no GPU:
+// span[2y] = first stored column of row y, span[2y+1] = -last (INT32_MAX,
+// INT32_MAX: none); threads 0 = the library's default. Not part of include/rtamd.h.
+int rtx_copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
+                   const int32_t *span, int32_t threads) {
+  if (!dc || !dt || !sc || !st || !span || W <= 0 || H <= 0) return set_err(RT_E_INVALID, "bad arguments");
+  rth::copy_spans(dc, dt, sc, st, W, H, span, threads);
   return RT_OK;
 }
 

@@ -11,6 +11,7 @@
 #include <limits>
 #include <unordered_map>
 #include <utility>
+#include <vector>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -1029,13 +1030,38 @@ void copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, in
     return v >= 1 && v <= 64 ? v : 16;
   }();
   if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), cap}));
-#pragma omp parallel for schedule(static) num_threads(threads) if (threads > 1)
-  for (int32_t y = 0; y < H; ++y) {
+  auto row = [&](int32_t y) {
     const int32_t lo = span[2 * y], hi = -span[2 * y + 1];
-    if (lo > hi || lo < 0 || hi >= W) continue;  // (no hit: INT32_MAX, INT32_MAX)
+    if (lo > hi || lo < 0 || hi >= W) return;  // (no hit: INT32_MAX, INT32_MAX)
     const size_t o = (size_t)y * (size_t)W + (size_t)lo, w = (size_t)(hi - lo + 1);
     std::memcpy(dc + o, sc + o, w * 4);
     std::memcpy(dt + o, st + o, w * 4);
+  };
+  if (threads <= 1) {
+    for (int32_t y = 0; y < H; ++y) row(y);
+    return;
+  }
+  // the spans sit in the rows the scene covers (the middle of the frame for
+  // the app's centred model), so equal row counts per thread leave most
+  // threads idle: thread k takes the rows where the running pixel count
+  // crosses [k, k+1) / threads of the total
+  thread_local std::vector<int64_t> pre;
+  pre.assign((size_t)H + 1, 0);
+  for (int32_t y = 0; y < H; ++y) {
+    const int32_t lo = span[2 * y], hi = -span[2 * y + 1];
+    pre[y + 1] = pre[y] + (lo > hi || lo < 0 || hi >= W ? 0 : (int64_t)(hi - lo + 1) + 16);
+  }
+  const int64_t total = pre[H];
+  if (total == 0) return;
+  const int64_t *pp = pre.data();
+#pragma omp parallel num_threads(threads)
+  {
+    const int k = omp_get_thread_num(), n = omp_get_num_threads();
+    const int64_t a = total * k / n, b = total * (k + 1) / n;
+    // rows y with a <= pre[y] < b start in this thread's share
+    const int32_t y0 = (int32_t)(std::lower_bound(pp, pp + H, a) - pp);
+    const int32_t y1 = (int32_t)(std::lower_bound(pp, pp + H, b) - pp);
+    for (int32_t y = y0; y < y1; ++y) row(y);
   }
 }
 
