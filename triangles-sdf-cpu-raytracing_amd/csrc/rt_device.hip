@@ -1279,6 +1279,7 @@ struct rt_scene {
   float *d_t = nullptr;
   size_t fb_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_host = nullptr;  // rt_render's pageable cleared frame: the spans are on the host
   hipStream_t xs[2] = {nullptr, nullptr};  // rt_render: colour / t copy streams (render on xs[0])
   hipEvent_t xev = nullptr;
   // rt_render: FrameArgs::hit_box of its frame (4 words) and a pinned,
@@ -1383,6 +1384,7 @@ int pick_maxd(int depth, int32_t &maxd) {
 int ensure_events(rt_scene *s) {
   if (!s->ev0) HIP_TRY(hipEventCreate(&s->ev0));
   if (!s->ev1) HIP_TRY(hipEventCreate(&s->ev1));
+  if (!s->ev_host) HIP_TRY(hipEventCreateWithFlags(&s->ev_host, hipEventDisableTiming));
   return RT_OK;
 }
 
@@ -1495,8 +1497,12 @@ int schedule_end(rt_scene *s, const FrameArgs &fa, uint32_t gx, uint32_t gy, hip
   return RT_OK;
 }
 
+// defer_end: the schedule's order_kernel is not queued; *defer_end receives
+// the frame's arguments for schedule_end_of (rt_render's pageable cleared
+// frame queues its span download first)
 int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
-                  unsigned long long *counters = nullptr, int diag = 0, bool sched = true) {
+                  unsigned long long *counters = nullptr, int diag = 0, bool sched = true,
+                  FrameArgs *defer_end = nullptr) {
   FrameArgs fa = fa_in;
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
   const uint32_t gx = (fa.W + kFTile - 1) / kFTile, gy = (fa.rows_local + kFTile - 1) / kFTile;
@@ -1535,8 +1541,18 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
     return set_err(RT_E_STATE, "scene has no geometry");
   }
   HIP_TRY(hipGetLastError());
-  if (diag == 0 && sched) return schedule_end(s, fa, gx, gy, stream);
+  if (diag == 0 && sched) {
+    if (defer_end) {
+      *defer_end = fa;
+      return RT_OK;
+    }
+    return schedule_end(s, fa, gx, gy, stream);
+  }
   return RT_OK;
+}
+
+int schedule_end_of(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
+  return schedule_end(s, fa, (fa.W + kFTile - 1) / kFTile, (fa.rows_local + kFTile - 1) / kFTile, stream);
 }
 
 // Work-queue heads of render_persist_kernel, one set per (device, stream):
@@ -2389,6 +2405,7 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->sched_ev) HIP_NOTE(hipEventDestroy(s->sched_ev));
   if (s->ev0) HIP_NOTE(hipEventDestroy(s->ev0));
   if (s->ev1) HIP_NOTE(hipEventDestroy(s->ev1));
+  if (s->ev_host) HIP_NOTE(hipEventDestroy(s->ev_host));
   if (s->xev) HIP_NOTE(hipEventDestroy(s->xev));
   if (s->d_hit_box) HIP_NOTE(hipFree(s->d_hit_box));
   if (s->h_hit_box) HIP_NOTE(hipHostFree(s->h_hit_box));
@@ -2572,6 +2589,16 @@ bool dropin_trace() {
   return on;
 }
 
+// The pageable drop-in's staging spans reset by the host threads that copy
+// them; RTAMD_HOST_CLEAR=0: by clear_spans_kernel instead (A/B switch).
+bool host_clears_stage() {
+  static const bool on = [] {
+    const char *e = std::getenv("RTAMD_HOST_CLEAR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // System-scope stores into host frames (kFlagHostFrame); RTAMD_HOST_STORES=agent
 // turns them off (A/B switch).
 bool host_sys_stores() {
@@ -2618,9 +2645,15 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
       return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
     }
     HIP_TRY(hipEventRecord(s->ev0, a));
-    if (int rc = launch_render(s, fa, a)) return rc;
+    FrameArgs fe;
+    fe.cost = nullptr;
+    if (int rc = launch_render(s, fa, a, nullptr, 0, true, &fe)) return rc;
     HIP_TRY(hipEventRecord(s->ev1, a));
-    HIP_TRY(hipStreamSynchronize(a));
+    // the next frame's tile order is queued behind the frame and not waited
+    // for (it touches no caller memory)
+    if (int rc = schedule_end_of(s, fe, a)) return rc;
+    HIP_TRY(hipEventSynchronize(s->ev1));
+    drain.on = false;
     if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
     return RT_OK;
   }
@@ -2676,23 +2709,34 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(s->ev0, a));
   s->stage_dirty = true;  // until its spans are cleared again below
-  if (int rc = launch_render(s, fa, a)) return rc;
+  FrameArgs fe;
+  fe.cost = nullptr;
+  if (int rc = launch_render(s, fa, a, nullptr, 0, true, &fe)) return rc;
   HIP_TRY(hipEventRecord(s->ev1, a));
   box_out_kernel<<<(unsigned)((2 * H + 255) / 256), 256, 0, a>>>(s->d_row_span, s->h_row_span_dev, 2 * H);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(s->ev_host, a));
+  // the next frame's tile order runs while the host copies
+  if (int rc = schedule_end_of(s, fe, a)) return rc;
   const auto h1 = std::chrono::steady_clock::now();
-  HIP_TRY(hipStreamSynchronize(a));
+  HIP_TRY(hipEventSynchronize(s->ev_host));
   const auto h2 = std::chrono::steady_clock::now();
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   // the stored spans to the caller (host threads; every other pixel of the
-  // caller's cleared frame already holds the staging frame's 0 / +inf), then
-  // the same spans of the staging frame cleared again by the GPU, in stream
-  // order before the next frame's kernel; the call does not wait for it
-  rth::copy_spans(color, t, s->stage_c, s->stage_t, W, H, s->h_row_span, 0);
+  // caller's cleared frame already holds the staging frame's 0 / +inf); the
+  // host resets the same spans of the staging frame as it goes (the GPU only
+  // stores into it, from the next call on), and the span words are reset in
+  // stream order before the next frame's kernel; the call does not wait for that
+  const bool host_clear = host_clears_stage();
+  rth::copy_spans(color, t, s->stage_c, s->stage_t, W, H, s->h_row_span, 0, host_clear);
   const auto h3 = std::chrono::steady_clock::now();
   drain.on = false;
-  clear_spans_kernel<<<(unsigned)H, 256, 0, a>>>((uint32_t *)sc, (float *)st, s->d_row_span, W);
-  HIP_TRY(hipGetLastError());
+  if (host_clear) {
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_row_span, 0x7FFFFFFF, (size_t)H * 2, a));
+  } else {
+    clear_spans_kernel<<<(unsigned)H, 256, 0, a>>>((uint32_t *)sc, (float *)st, s->d_row_span, W);
+    HIP_TRY(hipGetLastError());
+  }
   s->stage_dirty = false;
   if (dropin_trace()) {  // RTAMD_DROPIN_TRACE=1: host-side phases of this call (dev switch)
     const auto h4 = std::chrono::steady_clock::now();
@@ -3054,11 +3098,12 @@ int rtx_set_band_queue_px(int64_t px) {
 
 // The pageable drop-in's host copy (rth::copy_spans) on caller arrays, no GPU:
 // span[2y] = first stored column of row y, span[2y+1] = -last (INT32_MAX,
-// INT32_MAX: none); threads 0 = the library's default. Not part of include/rtamd.h.
-int rtx_copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
-                   const int32_t *span, int32_t threads) {
+// INT32_MAX: none); threads 0 = the library's default; clear_src != 0: the
+// copied spans of the source reset to (0, +inf). Not part of include/rtamd.h.
+int rtx_copy_spans(uint32_t *dc, float *dt, uint32_t *sc, float *st, int64_t W, int32_t H, const int32_t *span,
+                   int32_t threads, int32_t clear_src) {
   if (!dc || !dt || !sc || !st || !span || W <= 0 || H <= 0) return set_err(RT_E_INVALID, "bad arguments");
-  rth::copy_spans(dc, dt, sc, st, W, H, span, threads);
+  rth::copy_spans(dc, dt, sc, st, W, H, span, threads, clear_src != 0);
   return RT_OK;
 }
 

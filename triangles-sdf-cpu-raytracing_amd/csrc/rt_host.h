@@ -181,9 +181,10 @@ void copy_rect(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int
                int32_t y0, int32_t y1, int threads);
 // The same for per-row spans: row y's columns [span[2y], -span[2y+1]] (rows
 // with span[2y] > -span[2y+1] are skipped); rt_render's zero-copy cleared
-// frames on pageable buffers (FrameArgs::row_span).
-void copy_spans(uint32_t *dc, float *dt, const uint32_t *sc, const float *st, int64_t W, int32_t H,
-                const int32_t *span, int threads);
+// frames on pageable buffers (FrameArgs::row_span). clear_src: each copied
+// span of the source is then reset to the cleared frame (0, +inf).
+void copy_spans(uint32_t *dc, float *dt, uint32_t *sc, float *st, int64_t W, int32_t H, const int32_t *span,
+                int threads, bool clear_src = false);
 // FrameBuffer::clear() of n pixels (0, +inf), over up to `threads` threads.
 void clear_frame(uint32_t *c, float *t, int64_t n, int threads);
 
