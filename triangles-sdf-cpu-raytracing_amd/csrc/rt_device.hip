@@ -2617,15 +2617,15 @@ bool host_sys_stores() {
 //  * pageable buffers: into the scene's pinned staging frame, which is kept
 //    cleared. The kernel records, per row, the span of the pixels it stored
 //    (kFlagRowSpan); box_out_kernel moves the spans to mapped host memory, the
-//    host copies just those spans to the caller's buffers (OpenMP rows), and
-//    the GPU clears the same spans of the staging frame again
-//    (clear_spans_kernel), in stream order before the next frame.
+//    host copies just those spans to the caller's buffers (OpenMP rows) and
+//    resets them in the staging frame as it goes (RTAMD_HOST_CLEAR=0: the
+//    GPU does, clear_spans_kernel, in stream order before the next frame).
 int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *t, int32_t W, int32_t H,
                              float *ms) {
   const size_t px = (size_t)W * H;
   hipStream_t a = s->xs[0];
   // every return waits for stream a while it may still touch the caller's
-  // buffers; the staging frame's re-clear (below) is the library's own and
+  // buffers; the span-word reset (below) is the library's own and
   // is left running when the call returns
   struct Drain {
     hipStream_t a;
@@ -2658,7 +2658,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     return RT_OK;
   }
   if (px > s->stage_cap) {
-    HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's re-clear of the old frame)
+    HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's work on the old frame)
     stage_free(s);
     // pinned, mapped host memory the runtime owns: never handed back to the
     // process heap, so no caller buffer can later land on pages this library
@@ -2690,7 +2690,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     s->stage_dirty = true;  // (the spans of the frame in the staging frame are gone)
   }
   if (s->stage_dirty || s->stage_W != W || s->stage_H != H) {
-    // (otherwise the previous frame's clear_spans_kernel left both the staging
+    // (otherwise the previous frame's span reset left both the staging
     // frame and the span words reset)
     rth::clear_frame(s->stage_c, s->stage_t, (int64_t)px, 8);
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_row_span, 0x7FFFFFFF, (size_t)H * 2, a));
