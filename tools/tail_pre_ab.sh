@@ -1,6 +1,9 @@
 # last-frame prefix of the persistent launches (RTAMD_TAIL_PRE=<items>) vs off,
 # the driver's 20 frames as 10 x 2 and 128 frames as 8 x 2, interleaved rounds:
 # tools/tail_pre_ab.sh [outdir] [values]
+# The recipe of profiles/r05/tail_pre_ab.txt: the RTAMD_TAIL_PRE code was
+# measured level and removed, so on the shipping sources
+# every value runs the same kernel.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=${1:-gpurun_out/tail_pre}; mkdir -p $O
