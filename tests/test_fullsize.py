@@ -269,3 +269,37 @@ def test_config5_single_process_multi_device(gpu, devices, mode):
         torch.cuda.synchronize()
         assert_same((c, t), (cs[1].cpu().numpy().view(np.uint32), ts[1].cpu().numpy()),
                     f"rt_multi_render_device_frames {devices} {mode}")
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_fullsize_drop_in_cleared_frames(gpu, pinned):
+    """The app's frame loop at the headline size: FrameBuffer::clear() + draw
+    (rt_render, RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) on the same host buffers,
+    frame after frame around the orbit -- pageable buffers (hits stored into
+    the library's staging frame, the host copying and resetting the stored
+    row spans) or buffers pinned with rt_host_pin (hits stored straight into
+    them) -- each frame equal to the oracle's Renderer::draw bitwise
+    (raytracing.cpp:67-102, main.cpp:197-203)."""
+    from rtamd.workloads import orbit_positions
+    key = "bunny"
+    W, H = CASES[key]
+    rs, gs = scenes(key)
+    set_plane(key, "primary", rs, gs)
+    L = gpu.lib()
+    c = np.zeros((H, W), np.uint32)
+    t = np.full((H, W), np.inf, np.float32)
+    if pinned:
+        for a in (c, t):
+            gpu._lib.check(L.rt_host_pin(a.ctypes.data, a.nbytes))
+    try:
+        orbit = orbit_positions(64)
+        for k in (0, 5, 27, 6):
+            c[:] = 0
+            t[:] = np.inf
+            gs.render(S.params(key, W, H, "primary", orbit[k], "gpu"), c, t, cleared=True)
+            rc, rt_, _, _ = rs.render(S.params(key, W, H, "primary", orbit[k], "ref"), W, H)
+            assert_same((rc, rt_), (c, t), f"{key} {W}x{H} orbit {k} drop-in ({'pinned' if pinned else 'pageable'})")
+    finally:
+        if pinned:
+            L.rt_host_unpin(c.ctypes.data)
+            L.rt_host_unpin(t.ctypes.data)
