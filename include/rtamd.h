@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTAMD_ABI_VERSION 7
+#define RTAMD_ABI_VERSION 8
 
 enum rt_status {
   RT_OK = 0,
@@ -175,10 +175,17 @@ int rt_scene_get_plane(const rt_scene *s, int *enabled, float normal[3], float *
  * *ms (optional) receives the kernel time in milliseconds (HIP events). */
 int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t, int32_t W,
               int32_t H, uint32_t flags, float *ms);
-/* Pin (page-lock) a host framebuffer range for rt_render's DMA copies; the
- * caller keeps it pinned while it reuses the buffer (the reference app keeps
- * one FrameBuffer across frames, src/main.cpp:88) and unpins it before freeing
- * it. Optional: rt_render works on pageable memory too, through staged copies. */
+/* Pin (page-lock) a host framebuffer range, mapped on every device: rt_render
+ * and rt_multi_render then store a cleared frame's hits straight into it and
+ * DMA the other frames' copies directly. The caller keeps it pinned while it
+ * reuses the buffer (the reference app keeps one FrameBuffer across frames,
+ * src/main.cpp:88) and MUST unpin it before freeing it: a range freed while
+ * pinned stays mapped to its old pages, and a later buffer at the same address
+ * would be written through that stale mapping (rt_host_pin refuses a range
+ * that overlaps one still pinned). rt_host_unpin first drains every stream the
+ * library created. Optional: on pageable memory the library copies through its
+ * own pinned staging frames on the host, so the HIP runtime never DMAs from or
+ * to a caller's pageable memory. */
 int rt_host_pin(void *ptr, int64_t bytes);
 int rt_host_unpin(void *ptr);
 /* Same on DEVICE buffers, asynchronously on `stream` (hipStream_t or NULL).
@@ -236,10 +243,19 @@ int rt_multi_create(rt_scene *scene, const int32_t *devices, int32_t n, int32_t 
 int rt_multi_info(const rt_multi *m, int32_t *n, int32_t *exchange, int32_t *band_rows);
 /* Renderer::draw on HOST buffers, the same contract as rt_render (flags 0 =
  * tPrev frame, RT_FLAG_CLEAR, RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY). Blocks until
- * the assembled frame is in color / t. *ms (optional): device time from the
- * first launch to the assembled frame on the root (HIP events). */
+ * the frame is in color / t. The cleared frame (RT_FLAG_CLEAR |
+ * RT_FLAG_HITS_ONLY, the app's clear() + draw) takes no gather: every slot
+ * stores its bands' hits at their own rows straight into host memory (the
+ * caller's buffers when rt_host_pin pinned them, else a pinned staging frame
+ * whose stored spans the host copies). The other flags gather on the root.
+ * *ms (optional): device time from the first launch to the assembled frame
+ * (HIP events). */
 int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, float *t, int32_t W, int32_t H,
                     uint32_t flags, float *ms);
+/* Version code of the RCCL library rt_multi's gather runs on (ncclGetVersion:
+ * major * 10000 + minor * 100 + patch), i.e. whichever librccl the process
+ * resolved first (torch loads its own). */
+int rt_multi_rccl_version(int32_t *version);
 /* `frames` frames into DEVICE buffers on the root (d_color[f], d_t[f]),
  * flags must contain RT_FLAG_CLEAR. Stream-ordered on `stream` (a stream of
  * the root device, or NULL): the slots start after the work queued on it so

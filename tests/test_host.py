@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol(rt):
     assert not missing, missing
     # and the Python binding declares a signature for each of them
     assert set(names) == set(rt.EXPORTED)
-    assert rt.lib().rt_abi_version() == 7
+    assert rt.lib().rt_abi_version() == 8
 
 
 def test_library_build_id_matches_tree(rt):

@@ -53,6 +53,53 @@ def test_multi_matches_single_device(gpu, devices, band_rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("devices", [(0,), (0, 0), (0, 0, 0)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_multi_cleared_zero_copy(gpu, devices, pinned):
+    """The cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY, the app's clear()
+    + draw) takes no gather: every slot stores its bands' hits at their own rows
+    straight into host memory -- the caller's pinned buffers, or the handle's
+    staging frame whose stored spans the host copies. A sequence of frames
+    (sizes growing and shrinking, ragged band counts, cameras with no hit,
+    default and primary shading, band heights 8 and 3) equals rt_render's."""
+    import ctypes as C
+    rt = gpu
+    L = rt.lib()
+    name = "stanford-bunny.obj"
+    sc = S.gpu_scene(name)
+    seq = [(320, 180, "default", (0.0, 0.3, 2.5), 8), (333, 197, "primary", (0.2, 0.1, 0.9), 8),
+           (200, 120, "default", (0.0, 0.0, -30.0), 8), (400, 241, "default", (1.2, 0.4, 1.9), 3),
+           (333, 197, "primary", (-0.7, 0.5, 2.2), 3), (64, 7, "default", (0.1, 0.2, 2.4), 8)]
+    bufs = {}
+    try:
+        for W, H, mode, pos, br in seq:
+            if (W, H) not in bufs:
+                bufs[(W, H)] = (np.zeros((H, W), np.uint32), np.full((H, W), np.inf, np.float32))
+                if pinned:
+                    for a in bufs[(W, H)]:
+                        rt._lib.check(L.rt_host_pin(C.c_void_p(a.ctypes.data), a.nbytes))
+            c, t = bufs[(W, H)]
+            c[:] = 0
+            t[:] = np.inf
+            S.set_planes(name, mode, sc)
+            P = S.params(name, W, H, mode, pos, "gpu")
+            with rt.MultiRenderer(sc, devices, band_rows=br) as mr:
+                mr.render(P, c, t, cleared=True)
+                _eq((c, t), _frame(sc, P, W, H, {"clear": True}), f"{devices} {W}x{H} {mode} {pos} br {br}")
+                # a second frame on the same handle (staging frame and spans reused)
+                c[:] = 0
+                t[:] = np.inf
+                P2 = S.params(name, W, H, mode, (pos[0] + 0.3, pos[1], pos[2]), "gpu")
+                mr.render(P2, c, t, cleared=True)
+                _eq((c, t), _frame(sc, P2, W, H, {"clear": True}), f"{devices} {W}x{H} second frame")
+    finally:
+        if pinned:
+            for c, t in bufs.values():
+                L.rt_host_unpin(C.c_void_p(c.ctypes.data))
+                L.rt_host_unpin(C.c_void_p(t.ctypes.data))
+
+
+@pytest.mark.gpu
 def test_multi_against_oracle_and_plane_changes(gpu):
     """(0, 0): the assembled frame equals the oracle's Renderer::draw, and a
     plane set on the root scene after the handle was made reaches every slot."""

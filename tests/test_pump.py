@@ -7,10 +7,6 @@ zero direction components (the exact slab form), and 8 frames of different
 cameras mixed in one launch (lanes of one wave on different frames). The
 octrees and the SDF grid (linear 65^3 and the bricked 256^3 stand-in) are
 pumped."""
-import os
-import subprocess
-import sys
-
 import numpy as np
 import pytest
 import torch
@@ -18,7 +14,6 @@ import torch
 import scenes as S
 
 pytestmark = pytest.mark.gpu
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PUMPED = ["sdf_6.octree", "sdf_5.octree", "example_grid.grid"]
 
 
@@ -133,21 +128,27 @@ def test_pump_axis_aligned_cameras(gpu, name):
     same(batch(sc, prm, W, H), single(sc, prm, W, H), f"{name} axis-aligned")
 
 
-@pytest.mark.parametrize("refill", ["1", "8", "32", "64"])
-def test_pump_refill_thresholds(gpu, refill):
-    """Every refill threshold gives the same frames (run in a child process:
-    RTAMD_REFILL is read once per process)."""
-    code = (
-        "import sys; sys.path[:0] = [%r, %r, %r]\n"
-        "import torch, test_pump as T, scenes as S\n"
-        "sc = S.gpu_scene('sdf_6.octree'); sc.set_plane(None)\n"
-        "prm = T.cams(160, 96, 8, seed=4)\n"
-        "T.same(T.batch(sc, prm, 160, 96), T.single(sc, prm, 160, 96), 'refill')\n"
-        "print('ok')\n" % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
-                           os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd")))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RTAMD_REFILL=refill, RTAMD_PUMP="1"),
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+def refill(lanes):
+    """The pump's refill threshold (rtx_set_refill; 0 restores the default)."""
+    import ctypes as C
+
+    from rtamd import _lib
+    L = _lib.lib()
+    L.rtx_set_refill.argtypes = [C.c_int32]
+    _lib.check(L.rtx_set_refill(lanes))
+
+
+@pytest.mark.parametrize("lanes", [1, 8, 32, 64])
+def test_pump_refill_thresholds(gpu, lanes):
+    """Every refill threshold gives the same frames."""
+    sc = S.gpu_scene("sdf_6.octree")
+    sc.set_plane(None)
+    prm = cams(160, 96, 8, seed=4)
+    refill(lanes)
+    try:
+        same(batch(sc, prm, 160, 96), single(sc, prm, 160, 96), f"refill {lanes}")
+    finally:
+        refill(0)
 
 
 def test_pump_bricked_grid_stand_in(gpu):
@@ -161,16 +162,13 @@ def test_pump_bricked_grid_stand_in(gpu):
     same(batch(sc, prm, W, H), single(sc, prm, W, H), "grid 256^3")
 
 
-@pytest.mark.parametrize("refill", ["1", "32", "64"])
-def test_pump_grid_refill_thresholds(gpu, refill):
-    code = (
-        "import sys; sys.path[:0] = [%r, %r, %r]\n"
-        "import torch, test_pump as T, scenes as S\n"
-        "sc = S.gpu_scene('example_grid.grid'); sc.set_plane(None)\n"
-        "prm = T.cams(160, 96, 8, seed=5)\n"
-        "T.same(T.batch(sc, prm, 160, 96), T.single(sc, prm, 160, 96), 'refill')\n"
-        "print('ok')\n" % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
-                           os.path.join(ROOT, "triangles-sdf-cpu-raytracing_amd")))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RTAMD_REFILL=refill, RTAMD_PUMP="1"),
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+@pytest.mark.parametrize("lanes", [1, 32, 64])
+def test_pump_grid_refill_thresholds(gpu, lanes):
+    sc = S.gpu_scene("example_grid.grid")
+    sc.set_plane(None)
+    prm = cams(160, 96, 8, seed=5)
+    refill(lanes)
+    try:
+        same(batch(sc, prm, 160, 96), single(sc, prm, 160, 96), f"grid refill {lanes}")
+    finally:
+        refill(0)

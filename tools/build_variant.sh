@@ -18,7 +18,10 @@ if [ -n "$3" ]; then
   git -C $R show $3:include/rtamd.h > $S/include/rtamd.h
   SRC=$S/p/csrc/rt_device.hip
 fi
-HIPF=$(make -s print-hipflags)  # the shipping build's flags (the Makefile's HIPFLAGS)
+# the shipping build's flags (the Makefile's HIPFLAGS), plus RT_AB_ENV: a
+# variant reads the RTAMD_* A/B switches from the environment (the shipping
+# library does not, csrc/rt_host.h ab_env)
+HIPF="$(make -s print-hipflags) -DRT_AB_ENV=1"
 if [ "$VAR_UNIT" = bvhgpu ]; then
   /opt/rocm/bin/hipcc $HIPF $2 -c -o build/var/rt_bvhgpu_$1.o csrc/rt_bvhgpu.hip
   DEV=build/rt_device.o BVH=build/var/rt_bvhgpu_$1.o

@@ -845,7 +845,7 @@ __global__ void k_fill_tris(const uint32_t *tab, uint32_t nl, const float4 *vpos
 // RTAMD_BVH_TIMING=1: per-phase wall time of a device build on stderr (the
 // phases are synchronised for the measurement)
 struct PhaseTimer {
-  bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
+  bool on = ab_env("RTAMD_BVH_TIMING") != nullptr;
   double acc[8] = {};
   double host[4] = {};  // wall time of host-side stage sections (no syncs): prologue, FIFO, apply+boxes
   long faults[4] = {};  // minor page faults in those sections
@@ -1073,7 +1073,7 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   } while (0)
   // wall time of the whole call, teardown included (RTAMD_BVH_TIMING)
   struct WallClock {
-    bool on = std::getenv("RTAMD_BVH_TIMING") != nullptr;
+    bool on = ab_env("RTAMD_BVH_TIMING") != nullptr;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), tv = t0, te = t0;
     static double ms(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1161,8 +1161,9 @@ bool build_bvh8_gpu(const float *vpos4, int64_t nverts, const uint32_t *idx, int
   } sg{st};
   std::vector<uint32_t> iota(n);
   for (uint32_t t = 0; t < n; ++t) iota[t] = t;
-  BVH_DEV(hipMemcpyAsync(dv.p, vpos4, (size_t)nverts * 16, hipMemcpyHostToDevice, st), "upload");
-  BVH_DEV(hipMemcpyAsync(didx.p, idx, (size_t)nidx * 4, hipMemcpyHostToDevice, st), "upload");
+  // (the caller's arrays through rtdma: pinned memory only ever reaches the DMA)
+  BVH_DEV(rtdma::h2d(dv.p, vpos4, (size_t)nverts * 16, st), "upload");
+  BVH_DEV(rtdma::h2d(didx.p, idx, (size_t)nidx * 4, st), "upload");
   BVH_DEV(hipMemcpyAsync(ids3.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, st), "upload");
   k_tribox<<<(n + 255) / 256, 256, 0, st>>>(dv.p, didx.p, n, tbox.p, K3.p, KV3.p);
   BVH_DEV(hipGetLastError(), "triangle boxes");

@@ -55,7 +55,183 @@ std::string take_stale() {
   g_noted_err = hipSuccess;
   return m;
 }
+
+namespace {
+struct StreamInfo {
+  int device;
+  std::string label;
+  const char *last;  // the last library call that queued work on it (static strings)
+};
+std::mutex g_stream_mu;
+std::map<hipStream_t, StreamInfo> g_streams;
+
+// errors HIP keeps for the context once raised (a faulting kernel or copy):
+// every later call may report them, whichever work raised them
+bool sticky(hipError_t e) {
+  return e == hipErrorIllegalAddress || e == hipErrorLaunchFailure || e == hipErrorLaunchTimeOut ||
+         e == hipErrorAssert || e == hipErrorIllegalState || e == hipErrorUnknown;
+}
+}  // namespace
+
+void stream_add(hipStream_t s, int device, const std::string &label) {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  g_streams[s] = StreamInfo{device, label, "(nothing queued yet)"};
+}
+void stream_remove(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  g_streams.erase(s);
+}
+void stream_mark(hipStream_t s, const char *what) {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  auto it = g_streams.find(s);
+  if (it != g_streams.end()) it->second.last = what;
+}
+hipError_t streams_sync() {
+  std::vector<std::pair<hipStream_t, int>> all;
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    for (const auto &kv : g_streams) all.emplace_back(kv.first, kv.second.device);
+  }
+  int prev = 0;
+  if (const hipError_t e = hipGetDevice(&prev)) return e;
+  hipError_t first = hipSuccess;
+  for (const auto &[s, dev] : all) {
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess && first == hipSuccess) first = e;
+  }
+  (void)hipSetDevice(prev);
+  return first;
+}
+std::string stream_faults() {
+  std::vector<std::pair<hipStream_t, StreamInfo>> all;
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    for (const auto &kv : g_streams) all.emplace_back(kv.first, kv.second);
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  std::string m;
+  for (const auto &[s, info] : all) {
+    if (hipSetDevice(info.device) != hipSuccess) continue;
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess || e == hipErrorNotReady) continue;
+    m += (m.empty() ? "" : "; ") + info.label + " (device " + std::to_string(info.device) + ", last queued: " +
+         info.last + "): " + hipGetErrorName(e);
+  }
+  (void)hipSetDevice(prev);
+  (void)hipGetLastError();  // (the queries' errors are reported here, not left pending)
+  return m.empty() ? std::string("; no librtamd stream reports an error (the fault came from work queued "
+                                 "by this call itself or outside librtamd)")
+                   : "; librtamd streams reporting errors: " + m;
+}
+std::string hip_fail(const char *expr, hipError_t e) {
+  std::string m = std::string(expr) + ": " + hipGetErrorString(e);
+  if (sticky(e)) m += stream_faults();
+  return m;
+}
 }  // namespace rterr
+
+// ------------------------------------------------ caller host memory (rtdma) --
+namespace {
+// Host ranges pinned through rt_host_pin (base -> bytes): rt_render writes a
+// cleared frame's hits straight into such buffers, and rtdma DMAs them directly.
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pins;
+
+// The process-wide bounce buffer of rtdma: two halves of kBounce bytes of
+// pinned host memory (allocated on first use, kept for the process).
+constexpr size_t kBounce = 8u << 20;
+std::mutex g_bounce_mu;
+char *g_bounce[2] = {nullptr, nullptr};
+
+hipError_t bounce_ready() {
+  for (char *&b : g_bounce)
+    if (!b)
+      if (const hipError_t e = hipHostMalloc((void **)&b, kBounce, hipHostMallocPortable)) {
+        b = nullptr;
+        return e;
+      }
+  return hipSuccess;
+}
+}  // namespace
+
+namespace rtdma {
+void *pinned_device_ptr(const void *p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  uintptr_t base = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.upper_bound(a);
+    if (it == g_pins.begin()) return nullptr;
+    --it;
+    if (a < it->first || a + bytes > it->first + it->second) return nullptr;
+    base = it->first;
+  }
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, (void *)base, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();  // (not mapped: take the staged path)
+    return nullptr;
+  }
+  return (char *)d + (a - base);
+}
+bool pinned(const void *p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pins.upper_bound(a);
+  if (it == g_pins.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+hipError_t h2d(void *d, const void *h, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (pinned(h, n)) {
+    hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+  }
+  std::lock_guard<std::mutex> lk(g_bounce_mu);
+  if (const hipError_t e = bounce_ready()) return e;
+  // chunk k fills half k & 1 while the DMA of chunk k - 1 runs from the other
+  for (size_t off = 0, k = 0; off < n; off += kBounce, ++k) {
+    const size_t m = std::min(kBounce, n - off);
+    if (k >= 2)
+      if (const hipError_t e = hipStreamSynchronize(st)) return e;
+    std::memcpy(g_bounce[k & 1], (const char *)h + off, m);
+    if (const hipError_t e = hipMemcpyAsync((char *)d + off, g_bounce[k & 1], m, hipMemcpyHostToDevice, st)) {
+      (void)hipStreamSynchronize(st);
+      return e;
+    }
+  }
+  return hipStreamSynchronize(st);
+}
+hipError_t d2h(void *h, const void *d, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (pinned(h, n)) {
+    hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+  }
+  std::lock_guard<std::mutex> lk(g_bounce_mu);
+  if (const hipError_t e = bounce_ready()) return e;
+  // two chunks per round trip: both DMAs queued, then both copied out
+  for (size_t off = 0; off < n; off += 2 * kBounce) {
+    size_t m[2] = {0, 0};
+    for (int k = 0; k < 2 && off + k * kBounce < n; ++k) {
+      m[k] = std::min(kBounce, n - off - k * kBounce);
+      if (const hipError_t e = hipMemcpyAsync(g_bounce[k], (const char *)d + off + k * kBounce, m[k],
+                                              hipMemcpyDeviceToHost, st)) {
+        (void)hipStreamSynchronize(st);
+        return e;
+      }
+    }
+    if (const hipError_t e = hipStreamSynchronize(st)) return e;
+    for (int k = 0; k < 2; ++k)
+      if (m[k]) std::memcpy((char *)h + off + k * kBounce, g_bounce[k], m[k]);
+  }
+  return hipSuccess;
+}
+}  // namespace rtdma
 
 namespace {
 
@@ -351,6 +527,12 @@ constexpr uint32_t kFlagRowSpan = 1u << 29;
 // Internal flag: the frame's eye rays take eye_ray_fast (fill_frame sets it
 // when fast_eye_ok holds for its projection and size).
 constexpr uint32_t kFlagFastEye = 1u << 28;
+// Internal flag: a row-band tile's rows are stored at their own rows of a full
+// W x H frame (as RT_FLAG_TILE_NATURAL) but with the frame's plain stores and
+// no peer fence: rt_multi_render's zero-copy slots, whose frame is one host
+// frame shared by every slot (the kernels' end-of-dispatch release before the
+// host's stream synchronisation covers their stores, as for rt_render's).
+constexpr uint32_t kFlagNatural = 1u << 27;
 __device__ __forceinline__ void peer_release(uint32_t flags) {
 #if RT_PEER_RELEASE
   if (flags & kSysStoreFlags) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -419,9 +601,9 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
       d = eye_ray(active ? xo : 0, y, fa.W, fa.H, fa.P.proj_inv, fa.P.view_inv);
     // packed band layout (rank-local row yl) or, with RT_FLAG_TILE_NATURAL, the
     // full frame's own row (a peer's frame mapped over xGMI)
-    const bool peer = (fa.flags & kSysStoreFlags) != 0;
+    const bool natural = (fa.flags & (kSysStoreFlags | kFlagNatural)) != 0;
     const bool sys = (fa.flags & (kSysStoreFlags | kFlagHostFrame)) != 0;
-    const int yb = peer ? yo : yl;
+    const int yb = natural ? yo : yl;
     // 32-bit pixel index (check_params caps W*H at 2^31): one register live
     // across the traversal instead of two
     const uint32_t idx = active ? (uint32_t)yb * (uint32_t)fa.W + (uint32_t)xo : 0u;
@@ -1391,12 +1573,17 @@ int ensure_events(rt_scene *s) {
 // rt_render's two copy/render streams (non-blocking: no implicit sync with
 // the null stream) and the event that orders the uploads before the kernel
 int ensure_copy_streams(rt_scene *s) {
-  for (hipStream_t &x : s->xs)
-    if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k)
+    if (!s->xs[k]) {
+      HIP_TRY(hipStreamCreateWithFlags(&s->xs[k], hipStreamNonBlocking));
+      char label[64];
+      std::snprintf(label, sizeof label, "scene %p stream %s", (void *)s, k ? "t" : "render/colour");
+      rterr::stream_add(s->xs[k], s->device, label);
+    }
   if (!s->xev) HIP_TRY(hipEventCreateWithFlags(&s->xev, hipEventDisableTiming));
   if (!s->d_hit_box) HIP_TRY(hipMalloc(&s->d_hit_box, 4 * sizeof(int32_t)));
-  if (!s->h_hit_box) {
-    HIP_TRY(hipHostMalloc(&s->h_hit_box, 4 * sizeof(int32_t), hipHostMallocMapped));
+  if (!s->h_hit_box_dev) {  // (guarded on the device address: a failed lookup is retried next call)
+    if (!s->h_hit_box) HIP_TRY(hipHostMalloc(&s->h_hit_box, 4 * sizeof(int32_t), hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer((void **)&s->h_hit_box_dev, s->h_hit_box, 0));
   }
   return RT_OK;
@@ -1448,6 +1635,31 @@ void stage_free(rt_scene *s) {
     }
   }
   s->stage_cap = 0;
+}
+
+// The scene's staging frame for px pixels: pinned, mapped host memory the
+// runtime owns (hipHostMalloc), never handed back to the process heap, so no
+// caller buffer can later land on pages this library registered and
+// unregistered (aligned_alloc + hipHostRegister did that in round 5). Used by
+// rt_render on pageable caller buffers: the zero-copy cleared frame stores its
+// hits into it, and the other frames' uploads / downloads go through it (host
+// copies on one side, DMA on the other). Its stream xs[0] is synchronised
+// before a smaller frame is replaced.
+int ensure_stage(rt_scene *s, size_t px) {
+  if (px <= s->stage_cap) return RT_OK;
+  if (s->xs[0]) HIP_TRY(hipStreamSynchronize(s->xs[0]));  // (the previous frame's work on the old frame)
+  if (s->xs[1]) HIP_TRY(hipStreamSynchronize(s->xs[1]));
+  stage_free(s);
+  for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
+    if (const hipError_t e = hipHostMalloc(q, px * 4, hipHostMallocDefault)) {
+      *q = nullptr;
+      stage_free(s);
+      return set_err(RT_E_DEVICE, std::string("staging frame: ") + hipGetErrorString(e));
+    }
+  }
+  s->stage_cap = px;
+  s->stage_dirty = true;
+  return RT_OK;
 }
 
 // Cost-ordered schedule state for a frame of grid gx x gy blocks on `stream`.
@@ -1609,7 +1821,7 @@ struct BandSched {
 std::map<std::pair<int, hipStream_t>, BandSched> g_band_sched;  // (under g_queue_mu)
 
 bool band_order_env() {
-  const char *e = std::getenv("RTAMD_BAND_ORDER");
+  const char *e = ab_env("RTAMD_BAND_ORDER");
   return e && e[0] == '1';
 }
 std::atomic<bool> g_band_order{band_order_env()};
@@ -1644,7 +1856,7 @@ int64_t g_persist_stamps_cap = 0;
 // RTAMD_PERSIST=0 selects the one-block-per-16x16-tile dispatch (A/B switch).
 bool persist_enabled() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_PERSIST");
+    const char *e = ab_env("RTAMD_PERSIST");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1662,13 +1874,13 @@ bool persist_enabled() {
 // rule (A/B switches).
 // (rtx_set_band_queue_px sets the pixel threshold at run time, for tests)
 std::atomic<int64_t> g_band_queue_px{[] {
-  const char *e = std::getenv("RTAMD_BAND_PERSIST_PX");
+  const char *e = ab_env("RTAMD_BAND_PERSIST_PX");
   return e ? (int64_t)std::atoll(e) : (int64_t)1000000;
 }()};
 bool band_takes_queue(const FrameArgs &f) {
   if (f.nranks <= 1) return true;
   static const int max_ranks = [] {
-    const char *e = std::getenv("RTAMD_BAND_PERSIST");
+    const char *e = ab_env("RTAMD_BAND_PERSIST");
     return e ? std::atoi(e) : -1;
   }();
   if (max_ranks >= 0) return f.nranks <= max_ranks;
@@ -1679,7 +1891,7 @@ bool band_takes_queue(const FrameArgs &f) {
 // the scene's default (A/B switch)
 int persist_group(int dflt) {
   static const int g = [] {
-    const char *e = std::getenv("RTAMD_PERSIST_G");
+    const char *e = ab_env("RTAMD_PERSIST_G");
     return e ? std::atoi(e) : 0;
   }();
   return (g == 1 || g == 2 || g == 4) ? g : dflt;
@@ -1699,7 +1911,7 @@ int resident_blocks(K kernel, int &blocks, int &dev_cached, int block = kBlock) 
     // switch: extra waves start as resident ones leave and exit at once when
     // the queue is drained)
     static const int oversub = [] {
-      const char *e = std::getenv("RTAMD_PERSIST_OVERSUB");
+      const char *e = ab_env("RTAMD_PERSIST_OVERSUB");
       const int v = e ? std::atoi(e) : 1;
       return v >= 1 && v <= 8 ? v : 1;
     }();
@@ -1718,7 +1930,7 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   if (const int rc = stream_queue(stream, &heads)) return rc;
   q.heads = heads;
   static const uint32_t stride = [] {
-    const char *e = std::getenv("RTAMD_QSTRIDE");
+    const char *e = ab_env("RTAMD_QSTRIDE");
     const int v = e ? std::atoi(e) : 0;
     return (uint32_t)((v >= 1 && v <= kHeadStrideMax) ? v : kHeadStride);
   }();
@@ -1730,7 +1942,7 @@ int make_queue(const FrameBatch &fb, int n, int group, int blocks, hipStream_t s
   q.items = q.per_frame * (uint32_t)n;
   // RTAMD_QMAP=band: banded item order per head (PersistQ::cpf)
   static const bool banded = [] {
-    const char *e = std::getenv("RTAMD_QMAP");
+    const char *e = ab_env("RTAMD_QMAP");
     return e && std::strcmp(e, "band") == 0;
   }();
   q.cpf = banded ? (q.per_frame + 7) / 8 : 0;
@@ -1760,19 +1972,17 @@ int launch_persist_t(rt_scene *s, const S &sc, const PlaneDev &pl, const FrameBa
 // for the pump; RTAMD_REFILL=<lanes> sets its refill threshold.
 bool pump_env() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_PUMP");
+    const char *e = ab_env("RTAMD_PUMP");
     return e && e[0] == '1';
   }();
   return on;
 }
-int refill_min() {
-  static const int v = [] {
-    const char *e = std::getenv("RTAMD_REFILL");
-    const int r = e ? std::atoi(e) : 0;
-    return (r >= 1 && r <= 64) ? r : RT_REFILL_MIN;
-  }();
-  return v;
-}
+std::atomic<int> g_refill{[] {
+  const char *e = ab_env("RTAMD_REFILL");
+  const int r = e ? std::atoi(e) : 0;
+  return (r >= 1 && r <= 64) ? r : RT_REFILL_MIN;
+}()};
+int refill_min() { return g_refill.load(std::memory_order_relaxed); }
 
 // scenes with a ray-pump adapter (primary-ray batches)
 template <class S>
@@ -1914,7 +2124,7 @@ int check_params(const rt_render_params *p, int32_t W, int32_t H) {
 // RTAMD_FAST_EYE=0 keeps the divisions (A/B switch)
 bool fast_eye_enabled() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_FAST_EYE");
+    const char *e = ab_env("RTAMD_FAST_EYE");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -2037,7 +2247,7 @@ template <class T>
 int upload_padded(T **dst, const T *src, size_t n, size_t pad, int64_t &bytes) {
   HIP_TRY(hipMalloc(dst, (n + pad) * sizeof(T)));
   HIP_TRY(hipMemset(*dst, 0, (n + pad) * sizeof(T)));
-  if (n) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  if (n) HIP_TRY(rtdma::h2d(*dst, src, n * sizeof(T), nullptr));
   bytes += (int64_t)((n + pad) * sizeof(T));
   return RT_OK;
 }
@@ -2046,7 +2256,7 @@ template <class T>
 int upload(T **dst, const T *src, size_t n, int64_t &bytes) {
   if (n == 0) n = 1;  // keep a valid pointer
   HIP_TRY(hipMalloc(dst, n * sizeof(T)));
-  if (src) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  if (src) HIP_TRY(rtdma::h2d(*dst, src, n * sizeof(T), nullptr));
   bytes += (int64_t)(n * sizeof(T));
   return RT_OK;
 }
@@ -2413,7 +2623,10 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->h_row_span) HIP_NOTE(hipHostFree(s->h_row_span));
   stage_free(s);
   for (hipStream_t x : s->xs)
-    if (x) HIP_NOTE(hipStreamDestroy(x));
+    if (x) {
+      rterr::stream_remove(x);
+      HIP_NOTE(hipStreamDestroy(x));
+    }
   HIP_NOTE(hipSetDevice(prev));
   delete s;
   return RT_OK;
@@ -2545,37 +2758,13 @@ std::atomic<int64_t> g_render_drains{0};
 
 namespace {
 
-// Host ranges pinned through rt_host_pin (base -> bytes): rt_render writes a
-// cleared frame's hits straight into such buffers.
-std::mutex g_pin_mu;
-std::map<uintptr_t, size_t> g_pins;
-
-// The device address of host range [p, p + bytes) when it lies inside one
-// range pinned by rt_host_pin, else nullptr.
-void *pinned_device_ptr(const void *p, size_t bytes) {
-  const uintptr_t a = (uintptr_t)p;
-  uintptr_t base = 0;
-  {
-    std::lock_guard<std::mutex> lk(g_pin_mu);
-    auto it = g_pins.upper_bound(a);
-    if (it == g_pins.begin()) return nullptr;
-    --it;
-    if (a < it->first || a + bytes > it->first + it->second) return nullptr;
-    base = it->first;
-  }
-  void *d = nullptr;
-  if (hipHostGetDevicePointer(&d, (void *)base, 0) != hipSuccess || !d) {
-    (void)hipGetLastError();  // (not mapped: take the staged path)
-    return nullptr;
-  }
-  return (char *)d + (a - base);
-}
+using rtdma::pinned_device_ptr;
 
 // RTAMD_DROPIN_ZC=0: rt_render's cleared frames take the device frame + boxed
 // download instead of the zero-copy path (A/B switch)
 bool dropin_zero_copy() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_DROPIN_ZC");
+    const char *e = ab_env("RTAMD_DROPIN_ZC");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -2583,7 +2772,7 @@ bool dropin_zero_copy() {
 
 bool dropin_trace() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_DROPIN_TRACE");
+    const char *e = ab_env("RTAMD_DROPIN_TRACE");
     return e && e[0] == '1';
   }();
   return on;
@@ -2593,7 +2782,7 @@ bool dropin_trace() {
 // them; RTAMD_HOST_CLEAR=0: by clear_spans_kernel instead (A/B switch).
 bool host_clears_stage() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_HOST_CLEAR");
+    const char *e = ab_env("RTAMD_HOST_CLEAR");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -2603,7 +2792,7 @@ bool host_clears_stage() {
 // turns them off (A/B switch).
 bool host_sys_stores() {
   static const bool on = [] {
-    const char *e = std::getenv("RTAMD_HOST_STORES");
+    const char *e = ab_env("RTAMD_HOST_STORES");
     return !(e && std::strcmp(e, "agent") == 0);
   }();
   return on;
@@ -2624,6 +2813,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
                              float *ms) {
   const size_t px = (size_t)W * H;
   hipStream_t a = s->xs[0];
+  rterr::stream_mark(a, "rt_render (zero-copy cleared frame)");
   // every return waits for stream a while it may still touch the caller's
   // buffers; the span-word reset (below) is the library's own and
   // is left running when the call returns
@@ -2657,23 +2847,7 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
     if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
     return RT_OK;
   }
-  if (px > s->stage_cap) {
-    HIP_TRY(hipStreamSynchronize(a));  // (the previous frame's work on the old frame)
-    stage_free(s);
-    // pinned, mapped host memory the runtime owns: never handed back to the
-    // process heap, so no caller buffer can later land on pages this library
-    // registered and unregistered (aligned_alloc + hipHostRegister did that;
-    // see DESIGN.md section 0d, the GPU-suite stop of round 5)
-    for (void **q : {(void **)&s->stage_c, (void **)&s->stage_t}) {
-      if (const hipError_t e = hipHostMalloc(q, px * 4, hipHostMallocDefault)) {
-        *q = nullptr;
-        stage_free(s);
-        return set_err(RT_E_DEVICE, std::string("staging frame: ") + hipGetErrorString(e));
-      }
-    }
-    s->stage_cap = px;
-    s->stage_dirty = true;
-  }
+  if (int rc = ensure_stage(s, px)) return rc;
   void *sc = nullptr, *st = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&sc, s->stage_c, 0));
   HIP_TRY(hipHostGetDevicePointer(&st, s->stage_t, 0));
@@ -2770,11 +2944,21 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   if ((rc = ensure_fb(s, px)) || (rc = ensure_events(s)) || (rc = ensure_copy_streams(s))) return rc;
   fa.color = s->d_color;
   fa.t = s->d_t;
-  // colour and t move on two streams (two DMA engines; concurrent when the host
-  // buffers are pinned, e.g. by rt_host_pin). Once a copy is queued, every
-  // return -- an error included -- first waits for both streams, so the caller
-  // may unpin or free its buffers as soon as the call returns.
+  // The DMA engines only ever see pinned memory (rtdma):
+  // buffers pinned by rt_host_pin are copied directly; pageable ones go through
+  // the scene's staging frame, host threads copying between it and the caller's
+  // buffers on the host side of each DMA (hc / ht: where the DMAs read / write).
+  const bool direct = rtdma::pinned(color, px * 4) && rtdma::pinned(t, px * 4);
+  if (!direct && (rc = ensure_stage(s, px))) return rc;
+  uint32_t *hc = direct ? color : s->stage_c;
+  float *ht = direct ? t : s->stage_t;
+  // colour and t move on two streams (two DMA engines, concurrent). Once a copy
+  // is queued, every return -- an error included -- first waits for both
+  // streams, so the caller may unpin or free its buffers as soon as the call
+  // returns.
   hipStream_t a = s->xs[0], b = s->xs[1];
+  rterr::stream_mark(a, "rt_render (render + colour copies)");
+  rterr::stream_mark(b, "rt_render (t copies)");
   struct Drain {
     hipStream_t a, b;
     ~Drain() {
@@ -2794,9 +2978,11 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   // written whole (a cleared frame) or uploaded whole (tPrev), so the box
   // holds exactly the caller's values outside the hits.
   const bool boxed = !(flags & RT_FLAG_CLEAR) || (flags & RT_FLAG_HITS_ONLY);
+  if (!direct) s->stage_dirty = true;  // (the zero-copy path's cleared staging frame is overwritten)
   if (!(flags & RT_FLAG_CLEAR)) {
-    HIP_TRY(hipMemcpyAsync(s->d_color, color, px * 4, hipMemcpyHostToDevice, a));
-    HIP_TRY(hipMemcpyAsync(s->d_t, t, px * 4, hipMemcpyHostToDevice, b));
+    if (!direct) rth::copy_rect(hc, ht, color, t, W, 0, W - 1, 0, H - 1, 0);
+    HIP_TRY(hipMemcpyAsync(s->d_color, hc, px * 4, hipMemcpyHostToDevice, a));
+    HIP_TRY(hipMemcpyAsync(s->d_t, ht, px * 4, hipMemcpyHostToDevice, b));
     HIP_TRY(hipEventRecord(s->xev, b));
     HIP_TRY(hipStreamWaitEvent(a, s->xev, 0));
   }
@@ -2811,32 +2997,36 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
   HIP_TRY(hipEventRecord(s->ev0, a));
   if ((rc = launch_render(s, fa, a))) return rc;
   HIP_TRY(hipEventRecord(s->ev1, a));
+  int32_t x0 = 0, x1 = W - 1, y0 = 0, y1 = H - 1;  // the region copied back
   if (!boxed) {
     HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
-    HIP_TRY(hipMemcpyAsync(t, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
-    HIP_TRY(hipMemcpyAsync(color, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
+    HIP_TRY(hipMemcpyAsync(ht, s->d_t, px * 4, hipMemcpyDeviceToHost, b));
+    HIP_TRY(hipMemcpyAsync(hc, s->d_color, px * 4, hipMemcpyDeviceToHost, a));
   } else {
     box_out_kernel<<<1, 64, 0, a>>>(s->d_hit_box, s->h_hit_box_dev, 4);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(a));
-    const int32_t x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
+    x0 = s->h_hit_box[0], x1 = -s->h_hit_box[1], y0 = s->h_hit_box[2], y1 = -s->h_hit_box[3];
     if (x0 <= x1 && y0 <= y1) {  // else: no hit, nothing changed
       HIP_TRY(hipStreamWaitEvent(b, s->ev1, 0));
       const size_t off = (size_t)y0 * W + x0, rows = (size_t)(y1 - y0 + 1), w = (size_t)(x1 - x0 + 1);
       if (w * 2 > (size_t)W) {  // wide box: whole rows, one contiguous copy per buffer
-        HIP_TRY(hipMemcpyAsync(t + (size_t)y0 * W, s->d_t + (size_t)y0 * W, rows * W * 4, hipMemcpyDeviceToHost, b));
-        HIP_TRY(hipMemcpyAsync(color + (size_t)y0 * W, s->d_color + (size_t)y0 * W, rows * W * 4,
+        x0 = 0;
+        x1 = W - 1;
+        HIP_TRY(hipMemcpyAsync(ht + (size_t)y0 * W, s->d_t + (size_t)y0 * W, rows * W * 4, hipMemcpyDeviceToHost, b));
+        HIP_TRY(hipMemcpyAsync(hc + (size_t)y0 * W, s->d_color + (size_t)y0 * W, rows * W * 4,
                                hipMemcpyDeviceToHost, a));
       } else {
-        HIP_TRY(hipMemcpy2DAsync(t + off, (size_t)W * 4, s->d_t + off, (size_t)W * 4, w * 4, rows,
+        HIP_TRY(hipMemcpy2DAsync(ht + off, (size_t)W * 4, s->d_t + off, (size_t)W * 4, w * 4, rows,
                                  hipMemcpyDeviceToHost, b));
-        HIP_TRY(hipMemcpy2DAsync(color + off, (size_t)W * 4, s->d_color + off, (size_t)W * 4, w * 4, rows,
+        HIP_TRY(hipMemcpy2DAsync(hc + off, (size_t)W * 4, s->d_color + off, (size_t)W * 4, w * 4, rows,
                                  hipMemcpyDeviceToHost, a));
       }
     }
   }
   HIP_TRY(hipStreamSynchronize(a));
   HIP_TRY(hipStreamSynchronize(b));
+  if (!direct && x0 <= x1 && y0 <= y1) rth::copy_rect(color, t, hc, ht, W, x0, x1, y0, y1, 0);
   if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
   return RT_OK;
 }
@@ -2851,7 +3041,21 @@ int64_t rtx_render_drain_count(void) { return g_render_drains.load(); }
 
 int rt_host_pin(void *ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad host range");
-  HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped));
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.upper_bound((uintptr_t)ptr + (size_t)bytes - 1);
+    if (it != g_pins.begin() && (--it)->first + it->second > (uintptr_t)ptr)
+      return set_err(RT_E_INVALID, "rt_host_pin: the range overlaps a range pinned earlier and not unpinned "
+                                   "(a buffer freed without rt_host_unpin?)");
+  }
+  // portable: mapped on every device (rt_multi_render's slots store into it)
+  const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    return set_err(RT_E_INVALID, "rt_host_pin: the HIP runtime already holds a registration over this range "
+                                 "(registered outside librtamd, or freed without unregistering)");
+  }
+  HIP_TRY(e);
   std::lock_guard<std::mutex> lk(g_pin_mu);
   g_pins[(uintptr_t)ptr] = (size_t)bytes;
   return RT_OK;
@@ -2861,8 +3065,13 @@ int rt_host_unpin(void *ptr) {
   if (!ptr) return set_err(RT_E_INVALID, "NULL pointer");
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
-    g_pins.erase((uintptr_t)ptr);
+    if (!g_pins.erase((uintptr_t)ptr)) return set_err(RT_E_INVALID, "rt_host_unpin: not a range pinned by rt_host_pin");
   }
+  // no library stream may still read or write the range when it is unregistered
+  // (every entry point drains its streams before returning; a failed call or a
+  // stream-ordered launch may not have)
+  if (const hipError_t e = rterr::streams_sync())
+    return set_err(RT_E_DEVICE, rterr::hip_fail("rt_host_unpin: draining the library's streams", e));
   HIP_TRY(hipHostUnregister(ptr));
   return RT_OK;
 }
@@ -2896,9 +3105,7 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
     if ((e = hipMalloc(&dO, n * 12)) || (e = hipMalloc(&dD, n * 12)) || (e = hipMalloc(&dT, n * 4)) ||
         (e = hipMalloc(&dN, n * 12)) || (e = hipMalloc(&dH, n * 4)) || (e = hipMalloc(&dP, n * 8)))
       break;
-    if ((e = hipMemcpy(dO, o, n * 12, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(dD, d, n * 12, hipMemcpyHostToDevice)))
-      break;
+    if ((e = rtdma::h2d(dO, o, n * 12, nullptr)) || (e = rtdma::h2d(dD, d, n * 12, nullptr))) break;
     if (s->kind == RT_SCENE_MESH) {
       MeshS sc{mesh_dev(s)};
       switch (s->maxd) {
@@ -2928,10 +3135,8 @@ int rt_intersect_rays(rt_scene *s, const float *o, const float *d, int64_t n, fl
       }
     }
     if ((e = hipGetLastError())) break;
-    if ((e = hipMemcpy(hit, dH, n * 4, hipMemcpyDeviceToHost)) ||
-        (e = hipMemcpy(t, dT, n * 4, hipMemcpyDeviceToHost)) ||
-        (e = hipMemcpy(normal, dN, n * 12, hipMemcpyDeviceToHost)) ||
-        (e = hipMemcpy(prim, dP, n * 8, hipMemcpyDeviceToHost)))
+    if ((e = rtdma::d2h(hit, dH, n * 4, nullptr)) || (e = rtdma::d2h(t, dT, n * 4, nullptr)) ||
+        (e = rtdma::d2h(normal, dN, n * 12, nullptr)) || (e = rtdma::d2h(prim, dP, n * 8, nullptr)))
       break;
   } while (0);
   cleanup();
@@ -3203,6 +3408,12 @@ int rtx_set_coop(rt_scene *s, int on) {
 // Diagnostic switch: primary-ray batches of this scene on the ray pump
 // (render_pump_kernel) instead of one tile per wave (default off).
 
+// the ray pump's refill threshold in lanes (1..64; other values: the default)
+int rtx_set_refill(int32_t lanes) {
+  g_refill.store((lanes >= 1 && lanes <= 64) ? lanes : RT_REFILL_MIN);
+  return RT_OK;
+}
+
 int rtx_set_pump(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   s->pump_on = on != 0;
@@ -3244,3 +3455,26 @@ int rt_bench_frames(rt_scene *s, const rt_render_params *params, int32_t frames,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------ rt_multi_render internals --
+namespace rti {
+// One slot of rt_multi_render's zero-copy cleared frame (RT_FLAG_CLEAR |
+// RT_FLAG_HITS_ONLY over a cleared host frame): the slot's bands of `tile` go
+// through the one-frame kernel on `stream`, storing only their hits, at their
+// own rows of the W x H host frame whose device addresses (on the scene's
+// device) are dc / dt (kFlagNatural: one frame shared by every slot). With
+// d_span != NULL the kernel records per LOCAL row (tile->rank's rows in
+// increasing order) the span of the pixels it stored (kFlagRowSpan, 2 words per
+// row, pre-set to INT32_MAX by the caller).
+int render_band_host(rt_scene *s, const rt_render_params *p, uint32_t *dc, float *dt, int32_t W, int32_t H,
+                     const rt_tile *tile, int32_t *d_span, hipStream_t stream) {
+  if (!s) return set_err(RT_E_INVALID, "scene is NULL");
+  if (int rc = check_params(p, W, H)) return rc;
+  FrameArgs fa;
+  if (int rc = fill_frame(fa, p, dc, dt, W, H, RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY, tile)) return rc;
+  if (fa.rows_local <= 0) return RT_OK;
+  fa.flags |= kFlagHostFrame | kFlagNatural | (d_span ? kFlagRowSpan : 0u);
+  fa.hit_box = d_span;
+  return launch_render(s, fa, stream);
+}
+}  // namespace rti

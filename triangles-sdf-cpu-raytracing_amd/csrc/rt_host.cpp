@@ -1038,12 +1038,12 @@ static void copy_words_stream(uint32_t *d, const uint32_t *s, size_t n) {
 void copy_spans(uint32_t *dc, float *dt, uint32_t *sc, float *st, int64_t W, int32_t H, const int32_t *span,
                 int threads, bool clear_src) {
   static const int cap = [] {  // RTAMD_COPY_THREADS: the thread cap (A/B switch)
-    const char *e = std::getenv("RTAMD_COPY_THREADS");
+    const char *e = ab_env("RTAMD_COPY_THREADS");
     const int v = e ? std::atoi(e) : 16;
     return v >= 1 && v <= 64 ? v : 16;
   }();
   static const bool nt = [] {  // RTAMD_COPY_NT=0: plain memcpy (A/B switch)
-    const char *e = std::getenv("RTAMD_COPY_NT");
+    const char *e = ab_env("RTAMD_COPY_NT");
     return !(e && e[0] == '0');
   }();
   if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), cap}));

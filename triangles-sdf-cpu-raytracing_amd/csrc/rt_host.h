@@ -5,11 +5,29 @@
 #pragma once
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 #include <utility>
 #include <vector>
 
 #include "rt_layout.h"
+
+// A/B and diagnostic switches (RTAMD_* environment variables) are read only
+// by variant builds (tools/build_variant.sh compiles with -DRT_AB_ENV=1): the
+// shipping librtamd.so ignores the environment, so a host application that
+// inherits one of them cannot change the render path. Run-time settings the
+// tests need have rtx_* setters instead.
+#ifndef RT_AB_ENV
+#define RT_AB_ENV 0
+#endif
+inline const char *ab_env(const char *name) {
+#if RT_AB_ENV
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 namespace rth {
 

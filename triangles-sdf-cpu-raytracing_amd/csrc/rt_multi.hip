@@ -20,6 +20,18 @@
 // on each slot's event). Pixels are independent and every slot renders its
 // bands with the single-device kernels, so an assembled frame is bitwise the
 // single-device frame (tests/test_multi.py).
+//
+// Host buffers (rt_multi_render). The reference app's frame loop is
+// frameBuf.clear(); draw() into host memory (src/main.cpp:196-207); that
+// cleared frame (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) takes no gather at all:
+// every slot's kernel stores its bands' hits at their own rows straight into
+// host memory, as rt_render's zero-copy path does on one device -- into the
+// caller's buffers when rt_host_pin pinned them (portable: mapped on every
+// device), else into the handle's pinned staging frame (kept cleared), whose
+// per-row spans of stored pixels the host then copies to the caller. The other
+// flags keep the device gather and move the caller's frame through the staging
+// frame on pageable buffers: the DMA only ever sees pinned memory (DESIGN.md
+// section 0e).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -30,6 +42,7 @@
 
 #include "../../include/rtamd.h"
 #include "rt_error.h"
+#include "rt_host.h"
 
 namespace {
 
@@ -71,6 +84,21 @@ struct rt_multi {
   float *rt = nullptr;
   uint32_t *fc = nullptr;  // root: one assembled frame for the host path
   float *ft = nullptr;
+  // host frames: the staging frame for pageable caller buffers (pinned, mapped
+  // on every device; kept cleared between zero-copy cleared frames while
+  // hs_dirty is false) and its address on each slot's device
+  uint32_t *hs_c = nullptr;
+  float *hs_t = nullptr;
+  size_t hs_cap = 0;
+  bool hs_dirty = true;
+  std::vector<uint32_t *> hs_c_dev;
+  std::vector<float *> hs_t_dev;
+  // zero-copy cleared frames on the staging frame: per slot, the span of
+  // stored pixels of each of its rows (2 words per local row, INT32_MAX when
+  // none) on its device and in pinned host memory; span_rows = rows per slot
+  std::vector<int32_t *> d_span, h_span;
+  int32_t span_rows = 0;
+  std::vector<int32_t> merged;  // the spans by image row
 };
 
 namespace {
@@ -96,6 +124,66 @@ void free_buffers(rt_multi *m) {
   m->rt = m->ft = nullptr;
   m->W = m->H = m->fcap = 0;
   m->cap = 0;
+}
+
+void free_host(rt_multi *m) {
+  for (int32_t i = 0; i < m->n; ++i) {
+    HIP_NOTE(hipSetDevice(m->dev[i]));
+    if (m->st[i]) HIP_NOTE(hipStreamSynchronize(m->st[i]));
+  }
+  for (int32_t i = 0; i < (int32_t)m->d_span.size(); ++i) {
+    HIP_NOTE(hipSetDevice(m->dev[i]));
+    if (m->d_span[i]) HIP_NOTE(hipFree(m->d_span[i]));
+    if (m->h_span[i]) HIP_NOTE(hipHostFree(m->h_span[i]));
+  }
+  m->d_span.assign(m->n, nullptr);
+  m->h_span.assign(m->n, nullptr);
+  m->span_rows = 0;
+  if (m->hs_c) HIP_NOTE(hipHostFree(m->hs_c));
+  if (m->hs_t) HIP_NOTE(hipHostFree(m->hs_t));
+  m->hs_c = nullptr;
+  m->hs_t = nullptr;
+  m->hs_cap = 0;
+  m->hs_c_dev.assign(m->n, nullptr);
+  m->hs_t_dev.assign(m->n, nullptr);
+}
+
+// the staging frame for px pixels (every slot stream is drained first when it grows)
+int ensure_host_stage(rt_multi *m, size_t px) {
+  if (px <= m->hs_cap) return RT_OK;
+  free_host(m);
+  const unsigned fl = hipHostMallocPortable | hipHostMallocMapped;
+  HIP_TRY(hipHostMalloc((void **)&m->hs_c, px * 4, fl));
+  HIP_TRY(hipHostMalloc((void **)&m->hs_t, px * 4, fl));
+  for (int32_t i = 0; i < m->n; ++i) {
+    HIP_TRY(hipSetDevice(m->dev[i]));
+    HIP_TRY(hipHostGetDevicePointer((void **)&m->hs_c_dev[i], m->hs_c, 0));
+    HIP_TRY(hipHostGetDevicePointer((void **)&m->hs_t_dev[i], m->hs_t, 0));
+  }
+  m->hs_cap = px;
+  m->hs_dirty = true;
+  return RT_OK;
+}
+
+// per-slot span buffers for `rows` rows per slot, set to INT32_MAX (no span)
+int ensure_spans(rt_multi *m, int32_t rows) {
+  if (rows <= m->span_rows) return RT_OK;
+  for (int32_t i = 0; i < m->n; ++i) {
+    HIP_TRY(hipSetDevice(m->dev[i]));
+    HIP_TRY(hipStreamSynchronize(m->st[i]));
+    if (m->d_span[i]) HIP_NOTE(hipFree(m->d_span[i]));
+    if (m->h_span[i]) HIP_NOTE(hipHostFree(m->h_span[i]));
+    m->d_span[i] = m->h_span[i] = nullptr;
+  }
+  m->span_rows = 0;
+  for (int32_t i = 0; i < m->n; ++i) {
+    HIP_TRY(hipSetDevice(m->dev[i]));
+    HIP_TRY(hipMalloc((void **)&m->d_span[i], (size_t)rows * 8));
+    HIP_TRY(hipMemsetD32((hipDeviceptr_t)m->d_span[i], 0x7FFFFFFF, (size_t)rows * 2));
+    HIP_TRY(hipHostMalloc((void **)&m->h_span[i], (size_t)rows * 8, hipHostMallocDefault));
+  }
+  m->span_rows = rows;
+  return RT_OK;
 }
 
 // buffers for `frames` frames (one chunk at most) of W x H
@@ -245,6 +333,10 @@ int rt_multi_create(rt_scene *scene, const int32_t *devices, int32_t n, int32_t 
   m->done.assign(n, nullptr);
   m->pc.assign(n, nullptr);
   m->pt.assign(n, nullptr);
+  m->hs_c_dev.assign(n, nullptr);
+  m->hs_t_dev.assign(n, nullptr);
+  m->d_span.assign(n, nullptr);
+  m->h_span.assign(n, nullptr);
   m->scene[0] = scene;
   std::vector<int> sorted(m->dev);
   std::sort(sorted.begin(), sorted.end());
@@ -255,6 +347,7 @@ int rt_multi_create(rt_scene *scene, const int32_t *devices, int32_t n, int32_t 
     if (rc != RT_OK) break;
     hipError_t e = hipSetDevice(m->dev[i]);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->st[i], hipStreamNonBlocking);
+    if (e == hipSuccess) rterr::stream_add(m->st[i], m->dev[i], "rt_multi slot " + std::to_string(i));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&m->done[i], hipEventDisableTiming);
     if (e == hipSuccess && i > 0 && m->dev[i] != m->dev[0]) {
       // peer copies and RCCL's transport between the slot and the root
@@ -309,7 +402,8 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
     return rterr::set(RT_E_INVALID, "rt_multi_render: RT_FLAG_HITS_ONLY needs RT_FLAG_CLEAR");
   DeviceGuard guard;
   if (int rc = sync_planes(m)) return rc;
-  if (int rc = ensure(m, W, H, 1, true)) return rc;
+  const size_t px = (size_t)W * H;
+  for (int32_t i = 0; i < m->n; ++i) rterr::stream_mark(m->st[i], "rt_multi_render");
   // once anything is queued every return waits for all slot streams, so the
   // caller's buffers are never read or written after the call returns
   struct Drain {
@@ -321,6 +415,89 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
       }
     }
   } drain{m};
+  // pinned caller buffers (rt_host_pin) are used directly; pageable ones go
+  // through the staging frame
+  bool direct = rtdma::pinned(color, px * 4) && rtdma::pinned(t, px * 4);
+  if (flags == (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY)) {
+    // the cleared frame, zero-copy: each slot stores its hits at their own
+    // rows of the host frame, no gather, no download
+    std::vector<uint32_t *> dc(m->n, nullptr);
+    std::vector<float *> dt(m->n, nullptr);
+    for (int32_t i = 0; i < m->n && direct; ++i) {
+      HIP_TRY(hipSetDevice(m->dev[i]));
+      dc[i] = (uint32_t *)rtdma::pinned_device_ptr(color, px * 4);
+      dt[i] = (float *)rtdma::pinned_device_ptr(t, px * 4);
+      direct = dc[i] && dt[i];
+    }
+    int32_t rows = 0;
+    if (!direct) {
+      if (int rc = ensure_host_stage(m, px)) return rc;
+      for (int32_t i = 0; i < m->n; ++i) {
+        const rt_tile tl = tile_of(m, i);
+        rows = std::max(rows, (int32_t)(rt_tile_pixels(W, H, &tl) / W));
+      }
+      if (int rc = ensure_spans(m, rows)) return rc;
+      if (m->hs_dirty) {  // (a cleared frame stays cleared: the host resets each copied span)
+        rth::clear_frame(m->hs_c, m->hs_t, (int64_t)px, 8);
+        m->hs_dirty = false;
+      }
+      for (int32_t i = 0; i < m->n; ++i) {
+        dc[i] = m->hs_c_dev[i];
+        dt[i] = m->hs_t_dev[i];
+      }
+    }
+    HIP_TRY(hipSetDevice(m->dev[0]));
+    HIP_TRY(hipEventRecord(m->ev0, m->st[0]));
+    if (!direct) m->hs_dirty = true;  // until the spans are copied and reset below
+    for (int32_t i = 0; i < m->n; ++i) {
+      HIP_TRY(hipSetDevice(m->dev[i]));
+      if (i > 0) HIP_TRY(hipStreamWaitEvent(m->st[i], m->ev0, 0));
+      const rt_tile tl = tile_of(m, i);
+      if (int rc = rti::render_band_host(m->scene[i], p, dc[i], dt[i], W, H, &tl, direct ? nullptr : m->d_span[i],
+                                         m->st[i]))
+        return rc;
+      if (!direct) {
+        const size_t r = (size_t)(rt_tile_pixels(W, H, &tl) / W);
+        HIP_TRY(hipMemcpyAsync(m->h_span[i], m->d_span[i], r * 8, hipMemcpyDeviceToHost, m->st[i]));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)m->d_span[i], 0x7FFFFFFF, r * 2, m->st[i]));
+      }
+      if (i > 0) HIP_TRY(hipEventRecord(m->done[i], m->st[i]));
+    }
+    HIP_TRY(hipSetDevice(m->dev[0]));
+    for (int32_t i = 1; i < m->n; ++i) HIP_TRY(hipStreamWaitEvent(m->st[0], m->done[i], 0));
+    HIP_TRY(hipEventRecord(m->ev1, m->st[0]));
+    for (int32_t i = 0; i < m->n; ++i) {
+      HIP_TRY(hipSetDevice(m->dev[i]));
+      HIP_TRY(hipStreamSynchronize(m->st[i]));
+    }
+    if (!direct) {
+      // the slots' spans by image row (slot i's local row yl is image row
+      // (yl / band_rows * n + i) * band_rows + yl % band_rows), then the stored
+      // spans to the caller, reset in the staging frame as they are copied
+      m->merged.assign((size_t)H * 2, 0x7FFFFFFF);
+      const int32_t br = m->band_rows;
+      for (int32_t i = 0; i < m->n; ++i) {
+        const rt_tile tl = tile_of(m, i);
+        const int32_t r = (int32_t)(rt_tile_pixels(W, H, &tl) / W);
+        for (int32_t yl = 0; yl < r; ++yl) {
+          const int32_t yo = m->n == 1 ? yl : (yl / br * m->n + i) * br + yl % br;
+          m->merged[2 * (size_t)yo] = m->h_span[i][2 * yl];
+          m->merged[2 * (size_t)yo + 1] = m->h_span[i][2 * yl + 1];
+        }
+      }
+      rth::copy_spans(color, t, m->hs_c, m->hs_t, W, H, m->merged.data(), 0, true);
+      m->hs_dirty = false;
+    }
+    if (ms) HIP_TRY(hipEventElapsedTime(ms, m->ev0, m->ev1));
+    return RT_OK;
+  }
+  if (int rc = ensure(m, W, H, 1, true)) return rc;
+  if (!direct) {
+    if (int rc = ensure_host_stage(m, px)) return rc;
+    m->hs_dirty = true;
+  }
+  uint32_t *hc = direct ? color : m->hs_c;  // where the DMAs read / write on the host
+  float *ht = direct ? t : m->hs_t;
   HIP_TRY(hipSetDevice(m->dev[0]));
   HIP_TRY(hipEventRecord(m->ev0, m->st[0]));
   const bool clear = (flags & RT_FLAG_CLEAR) != 0;
@@ -328,6 +505,7 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
     // tPrev frame (Renderer::draw over the caller's buffers, raytracing.cpp:
     // 89-94): every slot's packed buffers start as the caller's values of its
     // bands -- its full bands as one strided 2-D copy, a short last band apart
+    if (!direct) rth::copy_rect(hc, ht, color, t, W, 0, W - 1, 0, H - 1, 0);
     const size_t row = (size_t)W * 4;
     const int32_t nb = (H + m->band_rows - 1) / m->band_rows;
     for (int32_t i = 0; i < m->n; ++i) {
@@ -339,17 +517,17 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
         if ((int64_t)(b + 1) * m->band_rows <= H) ++full;
       const size_t band = row * m->band_rows, pitch = band * m->n;
       if (full > 0) {
-        HIP_TRY(hipMemcpy2DAsync(dc, band, (const char *)color + (size_t)i * band, pitch, band, full,
+        HIP_TRY(hipMemcpy2DAsync(dc, band, (const char *)hc + (size_t)i * band, pitch, band, full,
                                  hipMemcpyHostToDevice, m->st[i]));
-        HIP_TRY(hipMemcpy2DAsync(dt, band, (const char *)t + (size_t)i * band, pitch, band, full,
+        HIP_TRY(hipMemcpy2DAsync(dt, band, (const char *)ht + (size_t)i * band, pitch, band, full,
                                  hipMemcpyHostToDevice, m->st[i]));
       }
       const int32_t last = nb - 1;
       if (last % m->n == i && (int64_t)(last + 1) * m->band_rows > H) {  // the short last band is this slot's
         const size_t rows = (size_t)(H - last * m->band_rows);
-        HIP_TRY(hipMemcpyAsync((char *)dc + full * band, (const char *)color + (size_t)last * band, rows * row,
+        HIP_TRY(hipMemcpyAsync((char *)dc + full * band, (const char *)hc + (size_t)last * band, rows * row,
                                hipMemcpyHostToDevice, m->st[i]));
-        HIP_TRY(hipMemcpyAsync((char *)dt + full * band, (const char *)t + (size_t)last * band, rows * row,
+        HIP_TRY(hipMemcpyAsync((char *)dt + full * band, (const char *)ht + (size_t)last * band, rows * row,
                                hipMemcpyHostToDevice, m->st[i]));
       }
     }
@@ -359,12 +537,13 @@ int rt_multi_render(rt_multi *m, const rt_render_params *p, uint32_t *color, flo
   if (int rc = render_chunk(m, p, 1, oc, ot, clear ? RT_FLAG_CLEAR : 0u, true)) return rc;
   HIP_TRY(hipSetDevice(m->dev[0]));
   HIP_TRY(hipEventRecord(m->ev1, m->st[0]));
-  HIP_TRY(hipMemcpyAsync(color, m->fc, (size_t)W * H * 4, hipMemcpyDeviceToHost, m->st[0]));
-  HIP_TRY(hipMemcpyAsync(t, m->ft, (size_t)W * H * 4, hipMemcpyDeviceToHost, m->st[0]));
+  HIP_TRY(hipMemcpyAsync(hc, m->fc, px * 4, hipMemcpyDeviceToHost, m->st[0]));
+  HIP_TRY(hipMemcpyAsync(ht, m->ft, px * 4, hipMemcpyDeviceToHost, m->st[0]));
   for (int32_t i = 0; i < m->n; ++i) {
     HIP_TRY(hipSetDevice(m->dev[i]));
     HIP_TRY(hipStreamSynchronize(m->st[i]));
   }
+  if (!direct) rth::copy_rect(color, t, hc, ht, W, 0, W - 1, 0, H - 1, 0);
   if (ms) HIP_TRY(hipEventElapsedTime(ms, m->ev0, m->ev1));
   return RT_OK;
 }
@@ -396,15 +575,27 @@ int rt_multi_render_device_frames(rt_multi *m, const rt_render_params *params, i
   return RT_OK;
 }
 
+int rt_multi_rccl_version(int32_t *version) {
+  if (!version) return rterr::set(RT_E_INVALID, "rt_multi_rccl_version: NULL argument");
+  int v = 0;
+  NCCL_TRY(ncclGetVersion(&v));
+  *version = v;
+  return RT_OK;
+}
+
 int rt_multi_destroy(rt_multi *m) {
   if (!m) return RT_OK;
   DeviceGuard guard;
   free_buffers(m);
+  free_host(m);
   for (ncclComm_t c : m->comm)
     if (c) (void)ncclCommDestroy(c);
   for (int32_t i = 0; i < m->n; ++i) {
     HIP_NOTE(hipSetDevice(m->dev[i]));
-    if (m->st[i]) HIP_NOTE(hipStreamDestroy(m->st[i]));
+    if (m->st[i]) {
+      rterr::stream_remove(m->st[i]);
+      HIP_NOTE(hipStreamDestroy(m->st[i]));
+    }
     if (m->done[i]) HIP_NOTE(hipEventDestroy(m->done[i]));
     if (i > 0 && m->scene[i]) rt_scene_destroy(m->scene[i]);
   }

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kWave) void sdf_kernel(SdfDev m, const float *p3, i
 template <class T>
 int upload(T **d, const T *h, size_t n) {
   HIP_TRY(hipMalloc(reinterpret_cast<void **>(d), std::max<size_t>(n, 1) * sizeof(T)));
-  if (n) HIP_TRY(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
+  if (n) HIP_TRY(rtdma::h2d(*d, h, n * sizeof(T), nullptr));
   return RT_OK;
 }
 
@@ -228,7 +228,11 @@ constexpr int64_t kQueryBatch = 1 << 20;
 
 // The handle's query stream and staging for batches of up to `n` points.
 int query_staging(rt_sdf_mesh *m, int64_t n) {
-  if (!m->qs) HIP_TRY(hipStreamCreateWithFlags(&m->qs, hipStreamNonBlocking));
+  if (!m->qs) {
+    HIP_TRY(hipStreamCreateWithFlags(&m->qs, hipStreamNonBlocking));
+    rterr::stream_add(m->qs, m->device, "SDF query stream");
+  }
+  rterr::stream_mark(m->qs, "rt_sdf_mesh_points");
   const int64_t want = std::min(n, kQueryBatch);
   if (want <= m->q_cap) return RT_OK;
   HIP_TRY(hipStreamSynchronize(m->qs));
@@ -354,7 +358,7 @@ int rt_sdf_mesh_grid(rt_sdf_mesh *m, const uint32_t size[3], float *values) {
                      n, size[0], size[1], size[2], m->stack_cap, d);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(values, d, (size_t)n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = rtdma::d2h(values, d, (size_t)n * 4, nullptr);
   HIP_NOTE(hipFree(d));
   if (e != hipSuccess) return rterr::set(RT_E_DEVICE, std::string("sdf grid: ") + hipGetErrorString(e));
   return RT_OK;
@@ -384,6 +388,7 @@ int rt_sdf_mesh_destroy(rt_sdf_mesh *m) {
   HIP_NOTE(hipSetDevice(m->device));
   if (m->qs) {
     HIP_NOTE(hipStreamSynchronize(m->qs));
+    rterr::stream_remove(m->qs);
     HIP_NOTE(hipStreamDestroy(m->qs));
   }
   if (m->h_stage) HIP_NOTE(hipHostFree(m->h_stage));

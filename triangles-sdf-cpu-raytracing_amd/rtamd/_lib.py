@@ -88,6 +88,7 @@ _SIGS = {
                                   C.c_uint32, C.POINTER(C.c_float)]),
     "rt_multi_render_device_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                                 C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
+    "rt_multi_rccl_version": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_multi_destroy": (C.c_int, [C.c_void_p]),
     "rt_render": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                             C.c_uint32, C.POINTER(C.c_float)]),
