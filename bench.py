@@ -24,6 +24,13 @@ octree (configs[3]: depth-8 stand-in and the shipped sdf_6, both 3840x2160),
 configs[4]'s mesh on one GPU, and the bunny in the reference's DEFAULT shading
 mode (plane + Lambert + shadows + reflections; also reported as traced rays/s).
 
+Measured cache traffic (every workload): L1->L2 read requests
+(TCP_TCC_READ_REQ_sum) and L1 accesses (TCP_TOTAL_CACHE_ACCESSES_sum) in bytes,
+by the bytes per request / access of a calibration dispatch in the same
+rocprofv3 pass (calib_read_kernel: 256 MiB read once at 16 B per lane), over
+the same wall time -> roofline.measured; binding_roof / binding_frac = the
+largest MEASURED roof (DRAM, VALU issue, L2 reads).
+
 Roofline (every workload): achieved = ALGORITHMIC bytes per frame (the SURVEY
 8(d) byte model on the reference's data layout, counted exactly by the
 diagnostic variant of the same kernel over the same frames) / ms_per_step (the
@@ -57,7 +64,10 @@ last timed frame.
 
 drop_in (N=1): rt_render, the Renderer::draw surface INTEGRATION.md binds, on
 HOST buffers (upload when not cleared, render, download), ms per frame with the
-copies, on pageable and on pinned (rt_host_pin) buffers.
+copies, on pageable and on pinned (rt_host_pin) buffers; multi_rehearsal: the
+same for rt_multi_render with two slots on the one GPU. --single-process (and
+the N>1 run's single_process leg) reports rt_multi_render's host-buffer
+figures over its devices.
 
 cpu_baseline: the oracle (C++ restatement of the reference's CPU path, ISPC
 kernels as scalar C++) on every CPU this process is granted (see
@@ -423,7 +433,20 @@ def work_model(scene, params, tile, W, H):
     return per_frame, per_ray
 
 
-def roofline(algo_frame, ms_step, scene_bytes, ctr=None, pmc_err=None, group=8):
+def calib_bytes(calib):
+    """Bytes per L1->L2 read request and per L1 access on gfx950, from the
+    calibration dispatches (CALIB_MIB read once at 16 B/lane, every line missing
+    L1 exactly once): -> (bytes per TCP_TCC_READ_REQ, bytes per
+    TCP_TOTAL_CACHE_ACCESSES), or (None, None). MI355X_MICROARCH.md calibrates
+    only FETCH_SIZE / WRITE_SIZE ("other access widths are uncalibrated:
+    calibrate on a known byte count"), so these are measured in the same run."""
+    c = (calib or {}).get(16, {})
+    req, acc = c.get("TCP_TCC_READ_REQ_sum"), c.get("TCP_TOTAL_CACHE_ACCESSES_sum")
+    nbytes = CALIB_MIB << 20
+    return (nbytes / req if req else None), (nbytes / acc if acc else None)
+
+
+def roofline(algo_frame, ms_step, scene_bytes, ctr=None, pmc_err=None, group=8, calib=None):
     """The contract's roofline object for one workload, on the wall clock:
     achieved = algorithmic bytes per frame / ms_per_step; frac x peak x
     ms_per_step reproduces the bytes per frame. PMC counters (per launch of
@@ -455,8 +478,32 @@ def roofline(algo_frame, ms_step, scene_bytes, ctr=None, pmc_err=None, group=8):
     rl["valu_frac"] = round(issue, 4)
     rl["lane_util"] = round(lane, 4) if lane is not None else None
     rl["l2_hit"] = round(hits / (hits + miss), 4) if hits + miss else None
-    roofs = {"dram": dram / HBM_PEAK_GBS, "valu_issue": issue, "cache_bytes": achieved / L2_PEAK_GBS}
+    roofs = {"dram": dram / HBM_PEAK_GBS, "valu_issue": issue}
+    # measured cache traffic: L1->L2 read requests and L1 accesses, in bytes by
+    # the calibration dispatch's bytes per request / access, over the same time
+    bpr, bpa = calib_bytes(calib)
+    if bpr and "TCP_TCC_READ_REQ_sum" in ctr:
+        l2_read = ctr["TCP_TCC_READ_REQ_sum"] * bpr / group
+        l2_rate = l2_read / dur / 1e9
+        l1_acc = ctr.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0) / group
+        m = {"l2_read_bytes_per_frame": round(l2_read), "l2_read_GBs": round(l2_rate, 1),
+             "l2_read_frac": round(l2_rate / L2_PEAK_GBS, 4),
+             "l1_accesses_per_frame": round(l1_acc),
+             "l1_access_bytes_per_frame": round(l1_acc * bpa) if bpa else None,
+             "l1_access_GBs": round(l1_acc * bpa / dur / 1e9, 1) if bpa else None,
+             "algorithmic_over_l2_read": round(algo_frame / l2_read, 2) if l2_read else None,
+             "bytes_per_l2_read_req": round(bpr, 2), "bytes_per_l1_access": round(bpa, 2) if bpa else None,
+             "calibration": f"calib_read_kernel: {CALIB_MIB} MiB read once, 16 B per lane, same rocprofv3 pass"}
+        rl["measured"] = m
+        roofs["l2_read"] = l2_rate / L2_PEAK_GBS
+        if achieved > HBM_PEAK_GBS:
+            rl["algorithmic_note"] = (
+                f"algorithmic bytes arrive at {achieved / HBM_PEAK_GBS:.2f}x the HBM peak: they are cache hits "
+                f"(measured L2 read bytes are 1/{algo_frame / l2_read:.1f} of them, DRAM bytes "
+                f"{(fetch + write) / algo_frame * 100:.1f} %), so no byte roof binds this kernel")
     top = max(roofs, key=roofs.get)
+    rl["binding_roof"] = top
+    rl["binding_frac"] = round(roofs[top], 4)
     rl["binding"] = top if roofs[top] >= 0.5 else f"latency (largest roof {top} {roofs[top]:.2f})"
     return rl
 
@@ -483,6 +530,7 @@ PMC_PASSES = [
      "GRBM_GUI_ACTIVE"],
 ]
 PMC_LAUNCHES = 2
+CALIB_MIB, CALIB_WIDTHS = 256, (16, 4)  # L1/L2 counter calibration: MiB read once, bytes per lane
 
 
 def pmc_counters(keys, group):
@@ -501,7 +549,11 @@ def pmc_counters(keys, group):
         return {}, "rocprofv3 not found"
     env = dict(os.environ, TMPDIR="/tmp")
     plan = ",".join(f"{k}:{WORKLOADS[k][0]}:{WORKLOADS[k][1]}:{WORKLOADS[k][2]}:{WORKLOADS[k][3]}" for k in keys)
+    # the byte calibration of the L1 / L2 counters: one read pass of CALIB_MIB at
+    # 16 and at 4 bytes per lane (calib_read_kernel), in every pass
+    plan += "".join(f",calib:{w}:{CALIB_MIB}:0:-" for w in CALIB_WIDTHS)
     out = {k: {} for k in keys}
+    out["_calib"] = {w: {} for w in CALIB_WIDTHS}
     tmp = tempfile.mkdtemp(prefix="rtamd_pmc_", dir="/tmp")
     try:
         for i, ctrs in enumerate(PMC_PASSES):
@@ -512,14 +564,20 @@ def pmc_counters(keys, group):
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
             if r.returncode != 0:
                 return out, f"pass {ctrs[0]} rc={r.returncode}: {r.stderr[-200:]}"
-            rows = {}
+            rows, cal = {}, {}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if "render_" not in row["Kernel_Name"]:
+                        dst = rows if "render_" in row["Kernel_Name"] else \
+                            cal if "calib_read_kernel" in row["Kernel_Name"] else None
+                        if dst is None:
                             continue
-                        rows.setdefault(int(row["Dispatch_Id"]), {})[row["Counter_Name"]] = \
+                        dst.setdefault(int(row["Dispatch_Id"]), {})[row["Counter_Name"]] = \
                             float(row["Counter_Value"])
+            cdisp = [cal[k] for k in sorted(cal)]
+            if len(cdisp) == len(CALIB_WIDTHS):
+                for w, m in zip(CALIB_WIDTHS, cdisp):
+                    out["_calib"][w].update(m)
             disp = [rows[k] for k in sorted(rows)]
             if len(disp) != PMC_LAUNCHES * len(keys):
                 return out, f"pass {ctrs[0]}: {len(disp)} render dispatches, expected {PMC_LAUNCHES * len(keys)}"
@@ -545,14 +603,18 @@ def measure(key, entry, warmup, steps, streams, group, pmc, pmc_err, detail):
     _, _, (c1, t1) = run_single(scene, prm[warmup + steps - 1:], 0, 1, W, H, inflight=1)  # as the headline's check
     frame_ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
     algo, per_ray = work_model(scene, prm[warmup:], None, W, H)
-    rl = roofline(algo, ms_step, scene.device_bytes(), pmc.get(key), pmc_err, group)
+    rl = roofline(algo, ms_step, scene.device_bytes(), pmc.get(key), pmc_err, group, pmc.get("_calib"))
     one = one_stream_leg(scene, prm, warmup, steps, W, H, group, algo, rl["peak"], rl["peak_kind"]) \
         if streams > 1 else None
     out = {"config": cfg, "res": f"{W}x{H}", "mode": mode,
            "value": round(W * H * steps / wall / 1e6, 1), "ms_per_step": round(ms_step, 4),
            "frac": rl["frac"], "peak_kind": rl["peak_kind"],
            "dram_frac": rl.get("dram", {}).get("frac"), "valu_frac": rl.get("valu_frac"),
-           "lane_util": rl.get("lane_util"), "1stream_launch_ms": one["kernel_ms_per_launch"] if one else None,
+           "lane_util": rl.get("lane_util"),
+           "l2_read_bytes_per_frame": rl.get("measured", {}).get("l2_read_bytes_per_frame"),
+           "l2_read_frac": rl.get("measured", {}).get("l2_read_frac"),
+           "binding": rl.get("binding"), "binding_frac": rl.get("binding_frac"),
+           "1stream_launch_ms": one["kernel_ms_per_launch"] if one else None,
            "frame_check": frame_ok}
     if mode == "default":
         rays = per_ray.get("rays", 1.0)
@@ -611,6 +673,47 @@ def _drop_in_legs(scene, params, W, H, frames, L, out, np):
             if pinned:
                 L.rt_host_unpin(c.ctypes.data)
                 L.rt_host_unpin(t.ctypes.data)
+
+
+def drop_in_multi(scene, params, W, H, devices, frames=16):
+    """rt_multi_render (Renderer::draw over several GPUs of one process) on HOST
+    buffers, ms per frame including the copies, pageable and pinned: `cleared`
+    (the app's clear() + draw: every slot stores its hits at their own rows
+    straight into host memory, no gather), `clear` and `tprev` (the gather on
+    the root). At N = 1 the rehearsal runs two slots on the one GPU."""
+    import numpy as np
+    L = rtamd.lib()
+    out = {"devices": list(devices)}
+    with NoGC(), rtamd.MultiRenderer(scene, devices) as mr:
+        for pinned in (False, True):
+            c = np.zeros((H, W), np.uint32)
+            t = np.full((H, W), np.inf, np.float32)
+            if pinned:
+                rtamd._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+                rtamd._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+            try:
+                for how in ("cleared", "clear", "tprev"):
+                    kw = {"clear": how == "clear", "cleared": how == "cleared"}
+                    mr.render(params[0], c, t, **kw)  # warm
+                    wall, ks = 0.0, []
+                    for k in range(frames):
+                        if how == "cleared":  # the app's frameBuf.clear(), outside the timed call
+                            c.fill(0)
+                            t.fill(np.inf)
+                        t0 = time.perf_counter()
+                        ks.append(mr.render(params[k % len(params)], c, t, **kw))
+                        wall += time.perf_counter() - t0
+                    tag = "pinned" if pinned else "pageable"
+                    out[f"{tag}_{how}_ms"] = round(wall * 1e3 / frames, 4)
+                    if how == "cleared":
+                        out[f"{tag}_cleared_device_ms"] = round(statistics.median(ks), 4)
+            finally:
+                if pinned:
+                    L.rt_host_unpin(c.ctypes.data)
+                    L.rt_host_unpin(t.ctypes.data)
+    out["note"] = (f"rt_multi_render on host buffers, {W}x{H}, slots on devices {list(devices)}, ms/frame incl. "
+                   f"copies, {frames} frames each; *_device_ms: first launch to last slot done (HIP events)")
+    return out
 
 
 def cpu_scene(src):
@@ -727,6 +830,7 @@ def single_process_main(a, json_out):
     ok = bool(torch.equal(c1, lc) and torch.equal(t1.view(torch.int32), lt.view(torch.int32)))
     ms_step = wall * 1e3 / a.steps
     algo, _ = work_model(scene, params[a.warmup:a.warmup + min(a.steps, 64)], None, W, H)
+    dropin = None if a.no_drop_in else drop_in_multi(scene, params, W, H, devices)
     out = {
         "metric": METRIC, "value": round(W * H * a.steps / wall / 1e6, 1), "unit": "Mrays/s",
         "n_gpus": len(set(devices)), "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
@@ -743,6 +847,8 @@ def single_process_main(a, json_out):
         "exchange": exch, "slots": len(devices),
         "build_id": rtamd.lib().rt_build_id().decode(),
     }
+    if dropin is not None:
+        out["drop_in"] = dropin
     scene.close()
     print(json.dumps(out, separators=(",", ":")), file=json_out, flush=True)
     return 0 if ok else 1
@@ -768,7 +874,8 @@ def single_process_leg(a, world):
         return {"error": f"rc {r.returncode}: {(r.stderr or '')[-300:]}"}
     o = json.loads(lines[-1])
     return {"value": o["value"], "ms_per_step": o["ms_per_step"], "exchange": o["exchange"],
-            "slots": o["slots"], "frame_check": o["frame_check"], "parallelism": o["config"]["parallelism"]}
+            "slots": o["slots"], "frame_check": o["frame_check"], "parallelism": o["config"]["parallelism"],
+            "drop_in": o.get("drop_in")}
 
 
 def _free_port():
@@ -964,9 +1071,10 @@ def main():
     ms_step = wall * 1e3 / a.steps
     # algorithmic bytes of the WHOLE frame (every rank's bands) over the max-over-ranks wall time
     algo, per_ray = work_model(scene, params[a.warmup:a.warmup + min(a.steps, 64)], None, W, H)
-    rl = roofline(algo, ms_step, scene.device_bytes(), pmc.get(key), pmc_err, a.group)
+    rl = roofline(algo, ms_step, scene.device_bytes(), pmc.get(key), pmc_err, a.group, pmc.get("_calib"))
     detail["headline_work_per_ray"] = per_ray
     detail["headline_pmc_per_launch"] = pmc.get(key)
+    detail["pmc_calibration"] = {str(w): v for w, v in (pmc.get("_calib") or {}).items()}
     value = W * H * a.steps / wall / 1e6
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
@@ -1006,6 +1114,8 @@ def main():
         out["host_issue_ms_per_frame"] = round(rs.host_issue_s * 1e3 / a.steps, 4)
     if rank == 0 and not use_dist and not a.no_drop_in:
         out["drop_in"] = drop_in(scene, params, W, H)
+        # rt_multi_render's host-buffer path, rehearsed with two slots on this GPU
+        out["drop_in"]["multi_rehearsal"] = drop_in_multi(scene, params, W, H, [device, device])
     scene.close()
     if rank == 0 and not use_dist and not a.no_extra:
         out["extra"] = {k: measure(k, WORKLOADS[k], min(a.warmup, 16), min(a.steps, 64), a.streams, a.group, pmc,

@@ -7,7 +7,9 @@ are per dispatch), in the order given, so a reader can map the render-kernel
 dispatches to workloads by dispatch order.
 
 --plan key:src:W:H:mode[,key:src:W:H:mode...]  (src: a shipped input file or a
-stand-in key of rtamd.workloads.STANDINS; mode: primary | default)
+stand-in key of rtamd.workloads.STANDINS; mode: primary | default).
+calib:<width>:<MiB>:0:- issues one rtx_calib_read dispatch instead (the byte
+calibration of the L1/L2 counters, bench.py).
 """
 import argparse
 import os
@@ -51,6 +53,17 @@ def run(src, W, H, mode, group, launches):
     return ev[0].elapsed_time(ev[1]) / launches
 
 
+def calib(width, mib=256):
+    """rtx_calib_read: one read pass over `mib` MiB, `width` bytes per lane (the
+    PMC calibration dispatch, kernel calib_read_kernel)."""
+    import ctypes as C
+    L = rtamd.lib()
+    L.rtx_calib_read.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_uint32)]
+    sink = C.c_uint32(0)
+    rtamd._lib.check(L.rtx_calib_read(mib << 20, width, C.byref(sink)))
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--plan", default="bunny:stanford-bunny.obj:1920:1080:primary")
@@ -59,6 +72,10 @@ def main():
     a = ap.parse_args()
     for item in a.plan.split(","):
         key, src, W, H, mode = item.split(":")
+        if key == "calib":  # calib:<width>:<MiB>:0:- (one calibration dispatch)
+            calib(int(src), int(W))
+            print(f"calib: {W} MiB read at {src} B per lane", flush=True)
+            continue
         ms = run(src, int(W), int(H), mode, a.group, a.launches)
         print(f"{key} ({src} {W}x{H} {mode}): {ms:.4f} ms per launch of {a.group} frames", flush=True)
 

@@ -1294,6 +1294,18 @@ __global__ void clear_spans_kernel(uint32_t *c, float *t, int32_t *span, int32_t
 
 // rtx_rcp_check: out[0] += floats checked, out[1] += mismatches, out[2] = bits
 // of a mismatching x
+// rtx_calib_read: a grid-stride pass, each element loaded once; the xor of
+// everything is stored only if it equals a value a zeroed buffer never gives
+// (the loads cannot be dropped, and no store lands)
+__device__ __forceinline__ uint32_t fold(uint32_t v) { return v; }
+__device__ __forceinline__ uint32_t fold(uint4 v) { return v.x ^ v.y ^ v.z ^ v.w; }
+template <class T>
+__global__ __launch_bounds__(256) void calib_read_kernel(const T *__restrict__ p, int64_t n, uint32_t *out) {
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc ^= fold(p[i]);
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
 __global__ void rcp_check_kernel(uint32_t base, unsigned long long *out) {
   const uint32_t bits = base + blockIdx.x * blockDim.x + threadIdx.x;
   const float x = __uint_as_float(bits);
@@ -3333,6 +3345,38 @@ int rtx_rcp_check(uint64_t *checked, uint64_t *bad, uint32_t *first_bad) {
   *checked = h[0];
   *bad = h[1];
   *first_bad = (uint32_t)h[2];
+  return RT_OK;
+}
+
+// Diagnostic (bench.py's PMC calibration, tools/prof_frames.py): one pass of
+// calib_read_kernel over `bytes` of device memory, every byte loaded once
+// (`width` = 4 or 16 bytes per lane, consecutive lanes on consecutive
+// addresses), so the vector L1 misses every line exactly once and the
+// dispatch's TCP_TCC_READ_REQ / TCP_TOTAL_CACHE_ACCESSES counts give the bytes
+// per L1->L2 read request and per L1 access on gfx950. Not part of rtamd.h.
+int rtx_calib_read(int64_t bytes, int32_t width, uint32_t *sink) {
+  if (bytes <= 0 || (width != 4 && width != 16) || bytes % 1024) return set_err(RT_E_INVALID, "bad arguments");
+  void *d = nullptr;
+  uint32_t *o = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)bytes));
+  hipError_t e = hipMalloc(&o, 4);
+  if (e == hipSuccess) e = hipMemset(d, 0, (size_t)bytes);
+  if (e == hipSuccess) e = hipMemset(o, 0, 4);
+  if (e == hipSuccess) {
+    const int64_t n = bytes / width;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    if (width == 16)
+      calib_read_kernel<uint4><<<blocks, 256>>>((const uint4 *)d, n, o);
+    else
+      calib_read_kernel<uint32_t><<<blocks, 256>>>((const uint32_t *)d, n, o);
+    e = hipGetLastError();
+  }
+  uint32_t h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, o, 4, hipMemcpyDeviceToHost);
+  HIP_NOTE(hipFree(d));
+  if (o) HIP_NOTE(hipFree(o));
+  if (e != hipSuccess) return set_err(RT_E_DEVICE, std::string("calib read: ") + hipGetErrorString(e));
+  if (sink) *sink = h;
   return RT_OK;
 }
 
