@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <limits>
 #include <memory>
@@ -86,15 +87,23 @@ struct FrameBuffer {
   std::vector<uint32_t> color;
   std::vector<float> t;
   uint32_t w = 0, h = 0;
+  // true while the buffers hold clear()'s values (set by clear() / resize(),
+  // reset by Renderer::draw): draw then tells the library so (RT_FLAG_CLEAR |
+  // RT_FLAG_HITS_ONLY) -- the same image as the tPrev draw over a cleared
+  // frame, with nothing uploaded. A caller that writes color / t directly
+  // after clear() sets it to false.
+  bool cleared = false;
   void resize(uint32_t width, uint32_t height) {
     w = width;
     h = height;
     color.assign((size_t)w * h, 0u);
     t.assign((size_t)w * h, std::numeric_limits<float>::infinity());
+    cleared = true;
   }
   void clear() {
     std::fill(color.begin(), color.end(), 0u);
     std::fill(t.begin(), t.end(), std::numeric_limits<float>::infinity());
+    cleared = true;
   }
   uint32_t width() const { return w; }
   uint32_t height() const { return h; }
@@ -162,6 +171,10 @@ class IScene {
     if (!h_) throw Error(RT_E_STATE, "rtamd: scene not built");
     return h_.get();
   }
+  // Identity of the current device scene: a process-wide counter value taken
+  // at every (re)build, so a scene rebuilt at a freed scene's address is
+  // never mistaken for the old one (Renderer's multi-GPU handle keys on it).
+  uint64_t generation() const { return gen_; }
   // IScene::intersect for one ray (for many rays use intersect(n, ...)).
   HitInfo intersect(float3 o, float3 d, float tNear, float tFar) const {
     HitInfo r;
@@ -186,8 +199,13 @@ class IScene {
   struct Del {
     void operator()(rt_scene *s) const { rt_scene_destroy(s); }
   };
-  void reset(rt_scene *s) { h_.reset(s); }
+  void reset(rt_scene *s) {
+    static std::atomic<uint64_t> next{1};
+    h_.reset(s);
+    gen_ = next.fetch_add(1);
+  }
   std::unique_ptr<rt_scene, Del> h_;
+  uint64_t gen_ = 0;
 };
 
 // BVHBuilder::perform (triangles_raytracing.cpp:227-258): same SAH BVH8.
@@ -288,23 +306,30 @@ struct Renderer {
     p.enable_shadows = enableShadows;
     p.enable_reflections = enableReflections;
     float ms = 0.0f;
+    // over a frame that still holds clear()'s values (the viewer's loop,
+    // main.cpp:197-206) nothing needs uploading: the cleared-frame call
+    const uint32_t flags = fb.cleared ? (RT_FLAG_CLEAR | RT_FLAG_HITS_ONLY) : 0u;
     if (!devices.empty()) {
       check(rt_multi_render(multi(scene), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
-                            (int32_t)fb.height(), 0u, &ms));
-      return ms;
+                            (int32_t)fb.height(), flags, &ms));
+    } else {
+      check(rt_render(scene.handle(), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
+                      (int32_t)fb.height(), flags, &ms));
     }
-    check(rt_render(scene.handle(), &p, fb.color.data(), fb.t.data(), (int32_t)fb.width(),
-                    (int32_t)fb.height(), 0u, &ms));
+    fb.cleared = false;
     return ms;
   }
-  // the multi-GPU handle of (scene, devices, bandRows), made at first use
+  // the multi-GPU handle of (scene build, devices, bandRows), made at first
+  // use. Keyed on the scene's generation, not its address: its replicas on
+  // devices[1..] are copies of the scene as it was, so a rebuilt scene (a new
+  // perform / upload, possibly at a freed scene's address) gets a new handle.
   rt_multi *multi(const IScene &scene) const {
-    if (!multi_ || multi_scene_ != scene.handle() || multi_devices_ != devices || multi_rows_ != bandRows) {
+    if (!multi_ || multi_gen_ != scene.generation() || multi_devices_ != devices || multi_rows_ != bandRows) {
       multi_.reset();
       rt_multi *m = nullptr;
       check(rt_multi_create(scene.handle(), devices.data(), (int32_t)devices.size(), bandRows, &m));
       multi_.reset(m, MultiDel{});
-      multi_scene_ = scene.handle();
+      multi_gen_ = scene.generation();
       multi_devices_ = devices;
       multi_rows_ = bandRows;
     }
@@ -314,7 +339,7 @@ struct Renderer {
     void operator()(rt_multi *m) const { rt_multi_destroy(m); }
   };
   mutable std::shared_ptr<rt_multi> multi_;
-  mutable const rt_scene *multi_scene_ = nullptr;
+  mutable uint64_t multi_gen_ = 0;
   mutable std::vector<int32_t> multi_devices_;
   mutable int32_t multi_rows_ = 0;
 };
