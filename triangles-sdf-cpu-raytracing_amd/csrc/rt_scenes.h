@@ -322,12 +322,27 @@ constexpr int kCoopRays = RT_COOP_RAYS;
 #define RT_HEAVY_PRIO_LEVEL 3
 #endif
 
+// Primary mesh traversal (MAJ, mesh_primary_wave): an iteration whose lanes
+// split between leaf tests and inner expansions runs only the side with more
+// lanes -- the lanes of the side with fewer than 1/K as many wait one
+// iteration, their visit order unchanged -- so the wave mostly runs one of the
+// two branches per iteration instead of both. Modelled first on the CPU
+// (tools/trav_sim.cpp, bunny 1080p: 38 % of the kernel's iterations ran both
+// branches; waiting at K = 1 takes 14 % of the wave instructions for 15 % more
+// iterations), then measured (section 4, round 6): bunny 10 x 2 0.0808 /
+// 0.0800 -> 0.0777 / 0.0776, one frame 0.1806 -> 0.1594 / 0.1588 ms/frame. K =
+// 2 was level; the shading kernels (MAJ off) were ~2 % slower with it.
+// RT_MESH_MAJ = K (0: off everywhere; A/B switch).
+#ifndef RT_MESH_MAJ
+#define RT_MESH_MAJ 1
+#endif
+
 // The traversal loop. One iteration = one unit of this lane's work (expand a
 // node, test a leaf, or resume/pop a frame). (Measured and rejected: the
 // "while-while" split into an inner-node phase and a leaf phase: bunny
 // 0.342 -> 0.523 ms.) TAIL: before each iteration, if kCoopRays or fewer lanes
 // of the wave are still looping, store the state and return true (suspended).
-template <int BLOCK, bool ANY, bool FAST, bool TAIL, uint32_t LB = RT_LEAF_BATCH, class CT>
+template <int BLOCK, bool ANY, bool FAST, bool TAIL, uint32_t LB = RT_LEAF_BATCH, bool MAJ = false, class CT>
 __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                          LdsStack<BLOCK> st, MState &S, CT &cnt, int coop_rays = kCoopRays,
                                          int prio_iters = 0) {
@@ -343,6 +358,17 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       it = __builtin_amdgcn_readfirstlane(it + 1);
       if (it == prio_iters) __builtin_amdgcn_s_setprio(RT_HEAVY_PRIO_LEVEL);
     }
+#if RT_MESH_MAJ
+    if constexpr (MAJ && !ANY) {
+      // one branch per iteration where the lanes disagree by more than K to 1:
+      // the minority side's lanes wait (their visit order is unchanged, only
+      // later), so the wave runs the leaf test or the expansion, not both
+      const bool isL = word != rtl::kInvalidChild && (word & rtl::kLeafBit);
+      const bool isI = word != rtl::kInvalidChild && !(word & rtl::kLeafBit);
+      const uint32_t nL = (uint32_t)__popcll(__ballot(isL)), nI = (uint32_t)__popcll(__ballot(isI));
+      if ((isL && nL * RT_MESH_MAJ < nI) || (isI && nI * RT_MESH_MAJ < nL)) continue;
+    }
+#endif
     if (word != rtl::kInvalidChild) {
       if (word & rtl::kLeafBit) {
         float lt = kInf;
@@ -651,13 +677,13 @@ __device__ __forceinline__ bool mesh_primary_wave(const MeshDev &sc, f3 o, f3 d,
   }
   bool suspended = false;
   if (pending && sc.coop)
-    suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
-                                                                                  coop_rays, prio_iters)
-                     : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt,
-                                                                                   coop_rays, prio_iters);
+    suspended = fast ? mesh_run<BLOCK, false, true, true, RT_LEAF_BATCH_PRIMARY, true>(sc, o, d, inv, tNear, tFar, st, S,
+                                                                                        cnt, coop_rays, prio_iters)
+                     : mesh_run<BLOCK, false, false, true, RT_LEAF_BATCH_PRIMARY, true>(sc, o, d, inv, tNear, tFar, st, S,
+                                                                                         cnt, coop_rays, prio_iters);
   else if (pending)
-    (void)(fast ? mesh_run<BLOCK, false, true, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt)
-                : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY>(sc, o, d, inv, tNear, tFar, st, S, cnt));
+    (void)(fast ? mesh_run<BLOCK, false, true, false, RT_LEAF_BATCH_PRIMARY, true>(sc, o, d, inv, tNear, tFar, st, S, cnt)
+                : mesh_run<BLOCK, false, false, false, RT_LEAF_BATCH_PRIMARY, true>(sc, o, d, inv, tNear, tFar, st, S, cnt));
   // Rays still traversing: at most kCoopRays per branch of the fast/exact
   // dispatch above (each branch suspends on its own lane count), so up to
   // 2 * kCoopRays; they are finished 8 at a time (one per 8-lane group; a
