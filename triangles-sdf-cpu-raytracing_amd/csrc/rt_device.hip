@@ -766,11 +766,25 @@ constexpr int frame_block() { return DIAG == 0 ? kFBlock : kBlock; }
 template <int DIAG>
 constexpr int frame_tile() { return DIAG == 0 ? kFTile : kTile; }
 
+// one-frame kernel, mesh primary rays: wave priority after this many traversal
+// iterations and the cooperative tail's ray threshold (A/B switches; the
+// persistent kernel's are RT_HEAVY_PRIO and its own)
+#ifndef RT_FRAME_PRIO
+#define RT_FRAME_PRIO 0
+#endif
+#ifndef RT_FRAME_COOP
+#define RT_FRAME_COOP RT_COOP_RAYS
+#endif
 template <class S, int SLOTS, bool GENERAL, int DIAG>
 __global__ __launch_bounds__(frame_block<DIAG>()) __attribute__((amdgpu_waves_per_eu(min_waves<S, SLOTS, GENERAL, DIAG>())))
-void render_kernel(S sc, PlaneDev pl, FrameArgs fa,
+void render_kernel(S sc_arg, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
   __shared__ uint32_t stk[SLOTS * S::kFields * frame_block<DIAG>()];
+  S sc = sc_arg;
+  if constexpr (S::kCoop && !GENERAL && DIAG == 0) {
+    sc.prio_iters = RT_FRAME_PRIO;
+    sc.coop_rays = RT_FRAME_COOP;
+  }
   render_body<S, SLOTS, GENERAL, DIAG, frame_block<DIAG>()>(sc, pl, fa, counters, stk);
   peer_release(fa.flags);
 }
@@ -1387,28 +1401,11 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t c) {
   const uint32_t e = 32u - (uint32_t)__clz(c);
   return 2 * e + (e >= 2 ? (c >> (e - 2)) & 1u : 0u);
 }
-// The LDS atomics are aggregated per wave: most tiles of a frame share a few
-// cost classes (the background's above all), so one add per class present in a
-// wave's 64 tiles replaces up to 64 adds queued on one LDS word (one frame's
-// 8,160 tiles: 7.6 us per order_kernel before, round 6). The order within a
-// class is the atomics' order, as before: output-neutral either way.
 __global__ __launch_bounds__(1024) void order_kernel(uint32_t *cost, uint32_t *order, uint32_t n) {
   __shared__ uint32_t hist[kCostClasses];
-  const int lane = threadIdx.x & 63;
   for (uint32_t i = threadIdx.x; i < kCostClasses; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {  // (a uniform trip count: whole waves take part)
-    const uint32_t i = i0 + threadIdx.x;
-    const bool ok = i < n;
-    const uint32_t c = ok ? cost_class(cost[i]) : 0u;
-    for (uint64_t todo = __ballot(ok); todo;) {
-      const int leader = __ffsll((unsigned long long)todo) - 1;
-      const uint32_t cc = __shfl(c, leader, 64);
-      const uint64_t m = __ballot(ok && c == cc);
-      if (lane == leader) atomicAdd(&hist[cc], (uint32_t)__popcll(m));
-      todo &= ~m;
-    }
-  }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_class(cost[i])], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t run = 0;
@@ -1419,21 +1416,9 @@ __global__ __launch_bounds__(1024) void order_kernel(uint32_t *cost, uint32_t *o
     }
   }
   __syncthreads();
-  for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
-    const uint32_t i = i0 + threadIdx.x;
-    const bool ok = i < n;
-    const uint32_t c = ok ? cost_class(cost[i]) : 0u;
-    for (uint64_t todo = __ballot(ok); todo;) {
-      const int leader = __ffsll((unsigned long long)todo) - 1;
-      const uint32_t cc = __shfl(c, leader, 64);
-      const uint64_t m = __ballot(ok && c == cc);
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&hist[cc], (uint32_t)__popcll(m));
-      base = __shfl(base, leader, 64);
-      if (ok && c == cc) order[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
-      todo &= ~m;
-    }
-    if (ok) cost[i] = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    order[atomicAdd(&hist[cost_class(cost[i])], 1u)] = i;
+    cost[i] = 0;
   }
 }
 
@@ -1523,18 +1508,26 @@ struct rt_scene {
   size_t stage_cap = 0;
   int32_t stage_W = 0, stage_H = 0;
   bool stage_dirty = true;
-  // cost-ordered block schedule (see launch_render): per-block cost of the
-  // last frame rendered with sched_grid blocks, and the block order derived
-  // from it; sched_on = false renders in plain blockIdx order
-  uint32_t *d_cost = nullptr;
-  uint32_t *d_order = nullptr;
+  // cost-ordered block schedule (see launch_render), double-buffered: frame k
+  // of the scene's one-frame kernel records its tiles' costs into d_cost[k & 1]
+  // and dispatches in the order d_order[k & 1] that frame k - 2's costs gave;
+  // frame k's own order is computed by order_kernel on the side stream
+  // sched_os as soon as frame k is done (frame_ev), beside frame k + 1, and
+  // ord_ev[k & 1] marks it done. sched_key[b] = the grid (gx << 16 | gy) whose
+  // order d_order[b] holds (0: none). sched_on = false renders in plain
+  // blockIdx order
+  uint32_t *d_cost[2] = {nullptr, nullptr};
+  uint32_t *d_order[2] = {nullptr, nullptr};
+  uint32_t sched_key[2] = {0, 0};
+  bool ord_rec[2] = {false, false};
+  int sched_par = 0;
   uint32_t sched_cap = 0;
-  uint32_t sched_grid = 0;
   bool sched_on = true;
   bool coop = true;  // mesh primary rays: cooperative tail (rtx_set_coop)
-  hipStream_t sched_stream = nullptr;  // stream the schedule state was last used on
   hipStream_t last_stream = nullptr;   // stream of the previous frame (scheduled or not)
-  hipEvent_t sched_ev = nullptr;       // recorded after each order_kernel
+  hipStream_t sched_os = nullptr;      // side stream of the order kernels
+  hipEvent_t ord_ev[2] = {nullptr, nullptr};
+  hipEvent_t frame_ev = nullptr;
   bool pump_on = false;  // primary-ray batches on the ray pump (rtx_set_pump)
 };
 
@@ -1704,58 +1697,79 @@ int ensure_stage(rt_scene *s, size_t px) {
 }
 
 // Cost-ordered schedule state for a frame of grid gx x gy blocks on `stream`.
-// Renders of one scene on different streams are ordered through sched_ev, so
-// the order/cost buffers are never shared by two frames in flight.
+// Two cost / order buffer pairs alternate (rt_scene::d_cost): a frame waits
+// for the order kernel of two frames before (ord_ev of its parity: its order
+// is ready and its cost buffer zeroed), renders in that order, and its own
+// order kernel runs on the side stream after it, concurrently with the next
+// frame -- so back-to-back one-frame launches never queue behind an order
+// kernel (~8 us at 1080p), at the price of an order two frames old.
 int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
   fa.order = nullptr;
   fa.cost = nullptr;
   // Frames of this scene arriving on alternating streams are frames in flight:
-  // each one's tail is filled by the next frame's tiles, and an order_kernel
-  // between a stream's frames would serialise them (it needs a whole CU, which
-  // frees only when the other stream's frame drains). Such frames render in
+  // each one's tail is filled by the next frame's tiles. Such frames render in
   // blockIdx order and leave the schedule state alone.
   const bool same_stream = stream == s->last_stream;
   s->last_stream = stream;
   if (!s->sched_on || !same_stream) return RT_OK;
   const uint32_t nb = gx * gy;
+  if (!s->sched_os) {
+    HIP_TRY(hipStreamCreateWithFlags(&s->sched_os, hipStreamNonBlocking));
+    char label[64];
+    std::snprintf(label, sizeof label, "scene %p schedule stream", (void *)s);
+    rterr::stream_add(s->sched_os, s->device, label);
+    for (hipEvent_t &e : s->ord_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->frame_ev, hipEventDisableTiming));
+  }
   if (nb > s->sched_cap) {
-    if (s->d_cost) HIP_NOTE(hipFree(s->d_cost));
-    if (s->d_order) HIP_NOTE(hipFree(s->d_order));
-    s->d_cost = s->d_order = nullptr;
+    HIP_TRY(hipStreamSynchronize(s->sched_os));  // (no order kernel still reads the old buffers)
+    for (int b = 0; b < 2; ++b) {
+      if (s->d_cost[b]) HIP_NOTE(hipFree(s->d_cost[b]));
+      if (s->d_order[b]) HIP_NOTE(hipFree(s->d_order[b]));
+      s->d_cost[b] = s->d_order[b] = nullptr;
+      s->sched_key[b] = 0;
+    }
     s->sched_cap = 0;
-    s->sched_grid = 0;
-    if (s->sched_ev) HIP_TRY(hipEventSynchronize(s->sched_ev));
-    HIP_TRY(hipMalloc(&s->d_cost, (size_t)nb * 4));
-    HIP_TRY(hipMalloc(&s->d_order, (size_t)nb * 4));
-    HIP_TRY(hipMemset(s->d_cost, 0, (size_t)nb * 4));
+    for (int b = 0; b < 2; ++b) {
+      HIP_TRY(hipMalloc(&s->d_cost[b], (size_t)nb * 4));
+      HIP_TRY(hipMalloc(&s->d_order[b], (size_t)nb * 4));
+      HIP_TRY(hipMemset(s->d_cost[b], 0, (size_t)nb * 4));
+    }
     s->sched_cap = nb;
   }
-  if (!s->sched_ev) HIP_TRY(hipEventCreateWithFlags(&s->sched_ev, hipEventDisableTiming));
-  if (stream != s->sched_stream) {
-    HIP_TRY(hipStreamWaitEvent(stream, s->sched_ev, 0));
-    s->sched_stream = stream;
+  const int p = s->sched_par;
+  if (s->ord_rec[p]) {
+    // usually long done (it ran beside the previous frame): then no
+    // cross-stream barrier goes into the frame's stream
+    const hipError_t q = hipEventQuery(s->ord_ev[p]);
+    if (q == hipErrorNotReady) {
+      HIP_TRY(hipStreamWaitEvent(stream, s->ord_ev[p], 0));
+    } else if (q != hipSuccess) {
+      HIP_TRY(q);
+    }
   }
-  const uint32_t key = (gx << 16) | gy;
-  if (s->sched_grid == key) fa.order = s->d_order;
-  fa.cost = s->d_cost;
+  if (s->sched_key[p] == ((gx << 16) | gy)) fa.order = s->d_order[p];
+  fa.cost = s->d_cost[p];
   return RT_OK;
 }
 
+// the frame's order kernel on the side stream, after the frame
 int schedule_end(rt_scene *s, const FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
   if (!fa.cost) return RT_OK;
-  order_kernel<<<1, 1024, 0, stream>>>(s->d_cost, s->d_order, gx * gy);
+  const int p = s->sched_par;
+  HIP_TRY(hipEventRecord(s->frame_ev, stream));
+  HIP_TRY(hipStreamWaitEvent(s->sched_os, s->frame_ev, 0));
+  order_kernel<<<1, 1024, 0, s->sched_os>>>(s->d_cost[p], s->d_order[p], gx * gy);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(s->sched_ev, stream));
-  s->sched_grid = (gx << 16) | gy;
+  HIP_TRY(hipEventRecord(s->ord_ev[p], s->sched_os));
+  s->ord_rec[p] = true;
+  s->sched_key[p] = (gx << 16) | gy;
+  s->sched_par = p ^ 1;
   return RT_OK;
 }
 
-// defer_end: the schedule's order_kernel is not queued; *defer_end receives
-// the frame's arguments for schedule_end_of (rt_render's pageable cleared
-// frame queues its span download first)
 int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
-                  unsigned long long *counters = nullptr, int diag = 0, bool sched = true,
-                  FrameArgs *defer_end = nullptr) {
+                  unsigned long long *counters = nullptr, int diag = 0, bool sched = true) {
   FrameArgs fa = fa_in;
   const bool general = s->plane.on || fa.P.shading_mode != RT_SHADING_NORMAL;
   const uint32_t gx = (fa.W + kFTile - 1) / kFTile, gy = (fa.rows_local + kFTile - 1) / kFTile;
@@ -1794,18 +1808,8 @@ int launch_render(rt_scene *s, const FrameArgs &fa_in, hipStream_t stream,
     return set_err(RT_E_STATE, "scene has no geometry");
   }
   HIP_TRY(hipGetLastError());
-  if (diag == 0 && sched) {
-    if (defer_end) {
-      *defer_end = fa;
-      return RT_OK;
-    }
-    return schedule_end(s, fa, gx, gy, stream);
-  }
+  if (diag == 0 && sched) return schedule_end(s, fa, gx, gy, stream);
   return RT_OK;
-}
-
-int schedule_end_of(rt_scene *s, const FrameArgs &fa, hipStream_t stream) {
-  return schedule_end(s, fa, (fa.W + kFTile - 1) / kFTile, (fa.rows_local + kFTile - 1) / kFTile, stream);
 }
 
 // Work-queue heads of render_persist_kernel, one set per (device, stream):
@@ -2649,11 +2653,18 @@ int rt_scene_destroy(rt_scene *s) {
   // call or a caller-stream launch may not have)
   for (hipStream_t x : s->xs)
     if (x) HIP_NOTE(hipStreamSynchronize(x));
+  if (s->sched_os) HIP_NOTE(hipStreamSynchronize(s->sched_os));
   void *ptrs[] = {s->d_nodes, s->d_tris, s->d_vals, s->d_child, s->d_ovals, s->d_color, s->d_t,
-                  s->d_cost, s->d_order};
+                  s->d_cost[0], s->d_order[0], s->d_cost[1], s->d_order[1]};
   for (void *p : ptrs)
     if (p) HIP_NOTE(hipFree(p));
-  if (s->sched_ev) HIP_NOTE(hipEventDestroy(s->sched_ev));
+  for (hipEvent_t e : s->ord_ev)
+    if (e) HIP_NOTE(hipEventDestroy(e));
+  if (s->frame_ev) HIP_NOTE(hipEventDestroy(s->frame_ev));
+  if (s->sched_os) {
+    rterr::stream_remove(s->sched_os);
+    HIP_NOTE(hipStreamDestroy(s->sched_os));
+  }
   if (s->ev0) HIP_NOTE(hipEventDestroy(s->ev0));
   if (s->ev1) HIP_NOTE(hipEventDestroy(s->ev1));
   if (s->ev_host) HIP_NOTE(hipEventDestroy(s->ev_host));
@@ -2876,13 +2887,9 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
       return set_err(RT_E_DEVICE, "injected rt_render failure (rtx_render_inject_failure)");
     }
     HIP_TRY(hipEventRecord(s->ev0, a));
-    FrameArgs fe;
-    fe.cost = nullptr;
-    if (int rc = launch_render(s, fa, a, nullptr, 0, true, &fe)) return rc;
+    // (the frame's tile-order kernel runs on the schedule's side stream: not waited for)
+    if (int rc = launch_render(s, fa, a)) return rc;
     HIP_TRY(hipEventRecord(s->ev1, a));
-    // the next frame's tile order is queued behind the frame and not waited
-    // for (it touches no caller memory)
-    if (int rc = schedule_end_of(s, fe, a)) return rc;
     HIP_TRY(hipEventSynchronize(s->ev1));
     drain.on = false;
     if (ms) HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
@@ -2924,15 +2931,11 @@ int render_cleared_zero_copy(rt_scene *s, FrameArgs fa, uint32_t *color, float *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(s->ev0, a));
   s->stage_dirty = true;  // until its spans are cleared again below
-  FrameArgs fe;
-  fe.cost = nullptr;
-  if (int rc = launch_render(s, fa, a, nullptr, 0, true, &fe)) return rc;
+  if (int rc = launch_render(s, fa, a)) return rc;
   HIP_TRY(hipEventRecord(s->ev1, a));
   box_out_kernel<<<(unsigned)((2 * H + 255) / 256), 256, 0, a>>>(s->d_row_span, s->h_row_span_dev, 2 * H);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(s->ev_host, a));
-  // the next frame's tile order runs while the host copies
-  if (int rc = schedule_end_of(s, fe, a)) return rc;
   const auto h1 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventSynchronize(s->ev_host));
   const auto h2 = std::chrono::steady_clock::now();
@@ -3497,7 +3500,7 @@ int rtx_set_pump(rt_scene *s, int on) {
 int rtx_set_schedule(rt_scene *s, int on) {
   if (!s) return set_err(RT_E_INVALID, "scene is NULL");
   s->sched_on = on != 0;
-  s->sched_grid = 0;
+  s->sched_key[0] = s->sched_key[1] = 0;
   return RT_OK;
 }
 

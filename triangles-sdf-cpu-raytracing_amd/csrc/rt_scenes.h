@@ -1449,35 +1449,54 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
 // The front-to-back loop of intersectNode below the root. SUSPEND: before each
 // iteration, if `limit` or fewer lanes of the wave are still in the loop, save
 // the state and return RAY_PENDING.
+// Octree loop iterations whose lanes split between leaf marches and inner
+// expansions run only the side with more lanes (the others keep their chosen
+// child pending for the next iteration, their visit order unchanged), as the
+// mesh's primary loop does (RT_MESH_MAJ). 0: off (A/B switch).
+#ifndef RT_OCT_MAJ
+#define RT_OCT_MAJ 0
+#endif
+
 template <int BLOCK, bool FAST, bool SUSPEND, bool PACK, class CT>
 __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, float tNear, float tFar,
                                        LdsStack<BLOCK, kOctFields> st, OctRay &R, int limit, float &out_t,
                                        OctHitPt &hp, CT &cnt) {
   constexpr bool MASKS = !CT::kCounts;
+  constexpr bool MAJ = RT_OCT_MAJ && MASKS && !SUSPEND;
   uint32_t fbase = R.fbase, flist = R.lc & 0xFFFFFFu, fcnt = R.lc >> 24, leafm = R.leafm;
   OctXYZ<PACK> xyz(R.ix, R.iy, R.iz);
   int depth = R.depth, sp = R.sp;
+  uint32_t pj = 8;  // MAJ: the chosen child not visited yet (8: none)
   for (;;) {
     if (SUSPEND && __popcll(__ballot(1)) <= limit) {
       R = OctRay{fbase, flist | (fcnt << 24), leafm, xyz.ix(), xyz.iy(), xyz.iz(), depth, sp};
       return RAY_PENDING;
     }
-    if (fcnt == 0) {
-      if (sp == 0) return RAY_MISS;
-      --sp;
-      fbase = st.at(sp, 0);
-      const uint32_t lc = st.at(sp, 1);
-      const uint32_t w2 = st.at(sp, 2);  // leaf mask | depth << 8
-      if (MASKS) leafm = w2 & 0xFFu;
-      const int d2 = (int)(w2 >> 8);
-      xyz.up((uint32_t)(depth - d2));
-      depth = d2;
-      flist = lc & 0xFFFFFFu;
-      fcnt = lc >> 24;  // >= 1: empty frames are never pushed
+    if (!MAJ || pj == 8) {
+      if (fcnt == 0) {
+        if (sp == 0) return RAY_MISS;
+        --sp;
+        fbase = st.at(sp, 0);
+        const uint32_t lc = st.at(sp, 1);
+        const uint32_t w2 = st.at(sp, 2);  // leaf mask | depth << 8
+        if (MASKS) leafm = w2 & 0xFFu;
+        const int d2 = (int)(w2 >> 8);
+        xyz.up((uint32_t)(depth - d2));
+        depth = d2;
+        flist = lc & 0xFFFFFFu;
+        fcnt = lc >> 24;  // >= 1: empty frames are never pushed
+      }
+      pj = flist & 7u;
+      flist >>= 3;
+      fcnt -= 1;
     }
-    const uint32_t j = flist & 7u;
-    flist >>= 3;
-    fcnt -= 1;
+    const uint32_t j = pj;
+    if constexpr (MAJ) {
+      const bool lf = (leafm >> j) & 1u;
+      const uint32_t nL = (uint32_t)__popcll(__ballot(lf)), nI = (uint32_t)__popcll(__ballot(!lf));
+      if (lf ? nL < nI : nI < nL) continue;  // wait: j stays pending
+    }
+    pj = 8;
     const uint32_t cn = fbase + j;
     const OctXYZ<PACK> cxyz = xyz.child(j);
     rtl::OctWord cw{0u, 0u};
