@@ -217,7 +217,7 @@ int main(int argc, char **argv) {
   };
   Cost c[3];
   double both = 0, iters0 = 0, steps = 0;
-  long tiles = 0, busy_tiles = 0;
+  long tiles = 0, busy_tiles = 0, root_only = 0;
   for (int ty = 0; ty < H / 8; ++ty)
     for (int tx = 0; tx < W / 8; ++tx) {
       std::vector<std::string> seqs(64);
@@ -231,8 +231,12 @@ int main(int argc, char **argv) {
         any |= seqs[l].size() > 1;
       }
       ++tiles;
-      if (!any) continue;
+      if (!any) {  // (every ray ends at the root: one iteration of the root expansion)
+        for (int p = 0; p < 3; ++p) replay(seqs, p, cI, cL, cC, c[p]);
+        continue;
+      }
       ++busy_tiles;
+      for (int l = 0; l < 64; ++l) root_only += seqs[l].size() <= 1;
       for (int p = 0; p < 3; ++p) replay(seqs, p, cI, cL, cC, c[p]);
       // iterations of P0 that run both branches
       std::vector<size_t> pos2(64, 0);
@@ -245,8 +249,58 @@ int main(int argc, char **argv) {
         both += (nI && nL);
       }
     }
+  // P1 with lane refill (the ray pump): a wave streams the pixels of 2x1-tile
+  // items in queue order (every item of a row of items, frame rows top to
+  // bottom) and hands each finished lane the next pixel once >= R lanes are
+  // free; stream length = one row of items per wave
+  for (int R : {8, 16, 32}) {
+    Cost cr;
+    for (int ty = 0; ty < H / 8; ++ty) {
+      std::vector<std::string> stream;
+      for (int tx2 = 0; tx2 < W / 16; ++tx2)
+        for (int half = 0; half < 2; ++half)
+          for (int l = 0; l < 64; ++l) {
+            const int x = (tx2 * 2 + half) * 8 + (l & 7), yo = ty * 8 + (l >> 3), y = H - yo - 1;
+            const V3 d = eye(x, y);
+            const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            std::string sq;
+            trace(0, V3{pos[0], pos[1], pos[2]}, d, inv, 0.01f, 100.0f, sq);
+            stream.push_back(sq);
+          }
+      size_t next = 0;
+      std::vector<std::string> lane(64);
+      std::vector<size_t> at(64, 0);
+      std::vector<bool> live(64, false);
+      for (;;) {
+        int dead = 0;
+        for (int k = 0; k < 64; ++k) dead += !live[k];
+        if (dead >= R || next == 0)
+          for (int k = 0; k < 64 && next < stream.size(); ++k)
+            if (!live[k]) { lane[k] = stream[next++]; at[k] = 0; live[k] = !lane[k].empty(); }
+        int nI = 0, nL = 0, nlive = 0;
+        for (int k = 0; k < 64; ++k)
+          if (live[k]) { ++nlive; (lane[k][at[k]] == 'I' ? nI : nL)++; }
+        if (!nlive) { if (next >= stream.size()) break; continue; }
+        bool runI = nI > 0, runL = nL > 0;
+        if (runI && runL) { if (nL * g_k < nI) runL = false; else if (nI * g_k < nL) runI = false; }
+        cr.wave_instr += cC + (runI ? cI : 0) + (runL ? cL : 0);
+        cr.iters += 1;
+        for (int k = 0; k < 64; ++k) {
+          if (!live[k]) continue;
+          const char c = lane[k][at[k]];
+          if ((c == 'I' && runI) || (c == 'L' && runL)) {
+            cr.lane_instr += (c == 'I' ? cI : cL) + cC;
+            if (++at[k] >= lane[k].size()) live[k] = false;
+          }
+        }
+      }
+    }
+    std::printf("P1 + refill at %2d free lanes: lane util %.3f  wave instr %.4g  iterations %.4g  (x%.3f instr vs P1 per tile; whole frame)\n",
+                R, cr.lane_instr / (64.0 * cr.wave_instr), cr.wave_instr, cr.iters, cr.wave_instr / c[1].wave_instr);
+  }
   std::printf("tiles %ld (%ld with any ray past the root), steps per ray %.3f\n", tiles, busy_tiles,
               steps / ((double)W * H));
+  std::printf("rays of those tiles that end at the root: %.1f %%\n", 100.0 * root_only / (64.0 * busy_tiles));
   std::printf("P0 iterations running both branches: %.1f %%\n", 100.0 * both / iters0);
   const char *name[3] = {"P0 both branches (kernel)", "P1 minority side waits (K)", "P2 inner first"};
   for (int p = 0; p < 3; ++p)
