@@ -37,6 +37,7 @@ struct Node {
   uint32_t child[8];
 };
 
+bool g_split = false;  // leaves of more than 4 triangles as two iterations of one batch each
 std::vector<Node> nodes;
 std::vector<uint32_t> canon;
 std::vector<float> vpos;
@@ -103,7 +104,12 @@ float trace(uint32_t ni, V3 o, V3 d, V3 inv, float tn, float tf, std::string &se
   const Node &nd = nodes[ni];
   float best = INFINITY;
   if (nd.leaf) {
-    seq.push_back('L');
+    if (nd.n / 3 > 4) {
+      if (g_split) seq += "LL";
+      else seq.push_back('M');
+    } else {
+      seq.push_back('L');
+    }
     for (uint32_t k = 0; k < nd.n / 3; ++k) {
       const float t = tri(nd.start / 3 + k, o, d);
       if (t < best) best = t;
@@ -143,11 +149,12 @@ struct Cost {
 void replay(const std::vector<std::string> &s, int policy, double cI, double cL, double cC, Cost &out) {
   std::vector<size_t> pos(s.size(), 0);
   for (;;) {
-    int nI = 0, nL = 0, live = 0;
+    int nI = 0, nL = 0, live = 0, nM = 0;
     for (size_t k = 0; k < s.size(); ++k) {
       if (pos[k] >= s[k].size()) continue;
       ++live;
       (s[k][pos[k]] == 'I' ? nI : nL)++;
+      nM += s[k][pos[k]] == 'M';
     }
     if (!live) break;
     bool runI = nI > 0, runL = nL > 0;
@@ -158,7 +165,7 @@ void replay(const std::vector<std::string> &s, int policy, double cI, double cL,
     if (policy == 2 && runI) runL = false;
     double w = cC;
     if (runI) w += cI;
-    if (runL) w += cL;
+    if (runL) w += nM ? cL : cL / 2;  // a second batch of 4 triangles when any lane's leaf has more
     out.wave_instr += w;
     out.iters += 1;
     // lanes doing useful work: the common part for every lane that advances
@@ -166,8 +173,8 @@ void replay(const std::vector<std::string> &s, int policy, double cI, double cL,
     for (size_t k = 0; k < s.size(); ++k) {
       if (pos[k] >= s[k].size()) continue;
       const char c = s[k][pos[k]];
-      if ((c == 'I' && runI) || (c == 'L' && runL)) {
-        out.lane_instr += (c == 'I' ? cI : cL) + cC;
+      if ((c == 'I' && runI) || (c != 'I' && runL)) {
+        out.lane_instr += (c == 'I' ? cI : c == 'M' ? cL : cL / 2) + cC;
         ++pos[k];
         ++adv;
       }
@@ -184,6 +191,7 @@ int main(int argc, char **argv) {
   const double cI = argc > 4 ? std::atof(argv[4]) : 250, cL = argc > 5 ? std::atof(argv[5]) : 360,
                cC = argc > 6 ? std::atof(argv[6]) : 40;
   g_k = argc > 7 ? std::atof(argv[7]) : 1.0;
+  g_split = argc > 8 && std::atoi(argv[8]) != 0;
   int64_t nv = 0, ni = 0;
   if (rt_load_obj(obj, 1, nullptr, &nv, nullptr, &ni)) return std::printf("load: %s\n", rt_last_error()), 1;
   vpos.resize(4 * nv);
@@ -283,13 +291,15 @@ int main(int argc, char **argv) {
         if (!nlive) { if (next >= stream.size()) break; continue; }
         bool runI = nI > 0, runL = nL > 0;
         if (runI && runL) { if (nL * g_k < nI) runL = false; else if (nI * g_k < nL) runI = false; }
-        cr.wave_instr += cC + (runI ? cI : 0) + (runL ? cL : 0);
+        int nM = 0;
+        for (int k = 0; k < 64; ++k) nM += live[k] && lane[k][at[k]] == 'M';
+        cr.wave_instr += cC + (runI ? cI : 0) + (runL ? (nM ? cL : cL / 2) : 0);
         cr.iters += 1;
         for (int k = 0; k < 64; ++k) {
           if (!live[k]) continue;
           const char c = lane[k][at[k]];
-          if ((c == 'I' && runI) || (c == 'L' && runL)) {
-            cr.lane_instr += (c == 'I' ? cI : cL) + cC;
+          if ((c == 'I' && runI) || (c != 'I' && runL)) {
+            cr.lane_instr += (c == 'I' ? cI : c == 'M' ? cL : cL / 2) + cC;
             if (++at[k] >= lane[k].size()) live[k] = false;
           }
         }
