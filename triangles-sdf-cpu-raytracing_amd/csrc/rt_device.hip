@@ -1733,7 +1733,7 @@ int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStre
     for (int b = 0; b < 2; ++b) {
       HIP_TRY(hipMalloc(&s->d_cost[b], (size_t)nb * 4));
       HIP_TRY(hipMalloc(&s->d_order[b], (size_t)nb * 4));
-      HIP_TRY(hipMemset(s->d_cost[b], 0, (size_t)nb * 4));
+      HIP_TRY(hipMemsetAsync(s->d_cost[b], 0, (size_t)nb * 4, stream));  // (in the frame's stream order)
     }
     s->sched_cap = nb;
   }

@@ -179,7 +179,10 @@ int ensure_spans(rt_multi *m, int32_t rows) {
   for (int32_t i = 0; i < m->n; ++i) {
     HIP_TRY(hipSetDevice(m->dev[i]));
     HIP_TRY(hipMalloc((void **)&m->d_span[i], (size_t)rows * 8));
-    HIP_TRY(hipMemsetD32((hipDeviceptr_t)m->d_span[i], 0x7FFFFFFF, (size_t)rows * 2));
+    // in the slot's stream order: a plain hipMemsetD32 goes to the null stream,
+    // which the slot's non-blocking stream does not wait for (the first
+    // frame's kernel then met uninitialised span words: lost spans at 4K)
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)m->d_span[i], 0x7FFFFFFF, (size_t)rows * 2, m->st[i]));
     HIP_TRY(hipHostMalloc((void **)&m->h_span[i], (size_t)rows * 8, hipHostMallocDefault));
   }
   m->span_rows = rows;
