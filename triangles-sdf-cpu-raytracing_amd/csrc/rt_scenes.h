@@ -336,6 +336,9 @@ constexpr int kCoopRays = RT_COOP_RAYS;
 #ifndef RT_MESH_MAJ
 #define RT_MESH_MAJ 1
 #endif
+#ifndef RT_MESH_MAJ_DEN  // K = RT_MESH_MAJ / RT_MESH_MAJ_DEN
+#define RT_MESH_MAJ_DEN 1
+#endif
 
 // The traversal loop. One iteration = one unit of this lane's work (expand a
 // node, test a leaf, or resume/pop a frame). (Measured and rejected: the
@@ -366,7 +369,10 @@ __device__ __forceinline__ bool mesh_run(const MeshDev &sc, f3 o, f3 d, f3 inv, 
       const bool isL = word != rtl::kInvalidChild && (word & rtl::kLeafBit);
       const bool isI = word != rtl::kInvalidChild && !(word & rtl::kLeafBit);
       const uint32_t nL = (uint32_t)__popcll(__ballot(isL)), nI = (uint32_t)__popcll(__ballot(isI));
-      if ((isL && nL * RT_MESH_MAJ < nI) || (isI && nI * RT_MESH_MAJ < nL)) continue;
+      // wave-uniform: at most one side waits, so every iteration advances
+      const bool waitL = nL * RT_MESH_MAJ < nI * RT_MESH_MAJ_DEN;
+      const bool waitI = !waitL && nI * RT_MESH_MAJ < nL * RT_MESH_MAJ_DEN;
+      if ((isL && waitL) || (isI && waitI)) continue;
     }
 #endif
     if (word != rtl::kInvalidChild) {
