@@ -1,7 +1,9 @@
 # pageable / pinned drop-in: staging spans reset by the host copy threads vs
+# (the switches are read only by A/B builds: first `bash tools/build_variant.sh abenv ""`)
 # clear_spans_kernel (RTAMD_HOST_CLEAR), two interleaved rounds: tools/clear_ab.sh [outdir]
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export RTAMD_LIB=$PWD/triangles-sdf-cpu-raytracing_amd/lib/var_abenv.so
 O=${1:-gpurun_out/clear_ab}; mkdir -p $O
 for r in 1 2; do
   for hc in 1 0; do

@@ -1,6 +1,8 @@
 # drop-in phases (RTAMD_DROPIN_TRACE=1) inside the bench and tools/ab.py dropin: tools/dropin_diag.sh [outdir]
+# (the switches are read only by A/B builds: first `bash tools/build_variant.sh abenv ""`)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export RTAMD_LIB=$PWD/triangles-sdf-cpu-raytracing_amd/lib/var_abenv.so
 O=${1:-gpurun_out/dropin_diag}; mkdir -p $O
 for r in 1 2; do
   RTAMD_DROPIN_TRACE=1 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-extra --no-cpu-baseline --no-pmc > $O/bench_$r.log 2>&1

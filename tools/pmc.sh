@@ -1,13 +1,13 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run; no trace domains with --pmc).
-# usage: tools/pmc.sh <outdir> <workload> [frames] [frames per launch]
+# usage: tools/pmc.sh <outdir> <workload> [launches] [frames per launch]
 set -e
 OUT=${1:-gpurun_out/pmc}; WL=${2:-stanford-bunny.obj}; N=${3:-16}; G=${4:-1}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() { name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o p -- \
-    python3 tools/prof_frames.py --workload $WL --frames $N --group $G > $OUT/$name.log 2>&1 || { echo "pass $name failed"; tail -5 $OUT/$name.log; exit 1; }
+    python3 tools/prof_frames.py --plan "w:$WL:1920:1080:primary" --launches $N --group $G > $OUT/$name.log 2>&1 || { echo "pass $name failed"; tail -5 $OUT/$name.log; exit 1; }
 }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
