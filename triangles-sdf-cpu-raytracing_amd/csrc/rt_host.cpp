@@ -1037,15 +1037,11 @@ static void copy_words_stream(uint32_t *d, const uint32_t *s, size_t n) {
 
 void copy_spans(uint32_t *dc, float *dt, uint32_t *sc, float *st, int64_t W, int32_t H, const int32_t *span,
                 int threads, bool clear_src) {
-  static const int cap = [] {  // RTAMD_COPY_THREADS: the thread cap (A/B switch)
-    const char *e = ab_env("RTAMD_COPY_THREADS");
-    const int v = e ? std::atoi(e) : 16;
-    return v >= 1 && v <= 64 ? v : 16;
-  }();
-  static const bool nt = [] {  // RTAMD_COPY_NT=0: plain memcpy (A/B switch)
-    const char *e = ab_env("RTAMD_COPY_NT");
-    return !(e && e[0] == '0');
-  }();
+  // at most 16 threads (2-24 measured level, profiles/r05/dropin_threads.txt);
+  // streaming stores into the caller's frame (measured faster than memcpy,
+  // profiles/r05/dropin_copy_nt_ab.txt)
+  constexpr int cap = 16;
+  constexpr bool nt = true;
   if (threads <= 0) threads = std::max(1, std::min({H / 32, omp_get_max_threads(), cap}));
   auto row = [&](int32_t y) {
     const int32_t lo = span[2 * y], hi = -span[2 * y + 1];
