@@ -1153,6 +1153,11 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, float inv
 // start clamp as one v_med3 per axis (t1 is finite, so p is; the clamp's
 // result differs from std's only in the sign of a zero coordinate, which the
 // march's comparisons and oct_local's clamp never see).
+// 1: the leaf march as a one-exit loop (A/B switch; 0 the two-exit form)
+#ifndef RT_OCT_MARCH
+#define RT_OCT_MARCH 1
+#endif
+
 template <bool FAST, class CT>
 __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax,
                                          float inv_s, f3 o, f3 d, f3 inv, float tNear, float tFar,
@@ -1183,6 +1188,43 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   // The march's state (t, p, s) is all the loop carries; the hit is read off
   // it after the loop, so no output is a loop-carried value (the outputs
   // written inside the loop made the compiler copy ~13 registers per step).
+#if RT_OCT_MARCH
+  // One exit per step: the reference returns t + s at a hit and continues
+  // from t + s otherwise, so t advances on every step; the next point and
+  // its in-box test are computed on the hit step too (unused there). The
+  // point the hit was found at is rebuilt once after the loop from the t it
+  // was computed from: o + tp * d, clamped to the box -- on the first step
+  // that is the entry point as computed above, on a later one the clamp
+  // leaves it as it is (that point passed the in-box test; at most a zero
+  // coordinate's sign changes, which oct_local's clamp never sees). The
+  // two-exit form (a break on the hit, the box test as the loop condition)
+  // made the compiler carry the exit state in extra masks and copy t and p
+  // through 8 v_mov per step.
+  bool hit = false;
+  float tp = t;
+  if (inside(p)) {
+    bool in;
+    do {
+      const float s = oct_sdf(c, bmin, inv_s, p);
+      cnt.add(C_OCT_STEP, 1);
+      hit = s < 1e-4f;
+      tp = t;
+      t += s;
+      p = o + t * d;
+      in = inside(p);
+    } while (!hit && in);
+  }
+  if (hit) {
+    out_t = t;
+    const f3 q = o + tp * d;
+    if constexpr (FAST) {
+      out_p = f3{clamp_med3(q.x, bmin.x, bmax.x), clamp_med3(q.y, bmin.y, bmax.y), clamp_med3(q.z, bmin.z, bmax.z)};
+    } else {
+      out_p = vstd_min(vstd_max(q, bmin), bmax);
+    }
+  }
+  return hit;
+#else
   float s = 0.0f;
   bool in = inside(p);
   while (in) {
@@ -1198,6 +1240,7 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
     out_p = p;
   }
   return in;
+#endif
 }
 
 // Where a leaf march hit: the leaf (node index, integer box coordinates at
