@@ -1115,8 +1115,10 @@ __device__ __forceinline__ float oct_sdf(const OctCorners &c, f3 bmin, float inv
   const v2f t23 = v2f{c.v[2], c.v[3]} * b.x * a.y * zz;
   const v2f t45 = v2f{c.v[4], c.v[5]} * a.x * b.y * zz;
   const v2f t67 = v2f{c.v[6], c.v[7]} * a.x * a.y * zz;
-  float res = 0.0f;
-  res += t01.x;
+  // (the reference starts the sum from 0: 0 + x differs from x only for
+  // x = -0, and then only in the sign of an all-zero sum, which the march
+  // never sees -- s < 1e-4 either way, and t + s with t >= tNear > 0)
+  float res = t01.x;
   res += t01.y;
   res += t23.x;
   res += t23.y;
@@ -1158,12 +1160,25 @@ __device__ __forceinline__ f3 oct_normal(const OctCorners &c, f3 bmin, float inv
 #define RT_OCT_MARCH 1
 #endif
 
+// The box entry / exit of a node for FAST rays (bbox_intersection_fast), once
+// per visit: the leaf march starts from them and the inner expansion's
+// crossing-order path takes them as its P / Q (the same max / min of the same
+// slab distances, in another order: max and min are exact). 0 otherwise.
+template <bool FAST>
+__device__ __forceinline__ void oct_entry(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar, float &P,
+                                          float &Q) {
+  P = 0.0f;
+  Q = 0.0f;
+  if constexpr (FAST) bbox_intersection_fast(bmin, bmax, o, inv, tNear, tFar, P, Q);
+}
+
+// P, Q: oct_entry's values (FAST; ignored otherwise)
 template <bool FAST, class CT>
 __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmin, f3 bmax,
                                          float inv_s, f3 o, f3 d, f3 inv, float tNear, float tFar,
-                                         float &out_t, f3 &out_p, CT &cnt) {
-  float t1, t2;
-  bbox_isect<FAST>(bmin, bmax, o, inv, tNear, tFar, t1, t2);
+                                         float P, float Q, float &out_t, f3 &out_p, CT &cnt) {
+  float t1 = P, t2 = Q;
+  if constexpr (!FAST) bbox_isect<FAST>(bmin, bmax, o, inv, tNear, tFar, t1, t2);
   if (t1 > t2) return false;
   OctCorners c;
   const float4 *q = reinterpret_cast<const float4 *>(sc.vals + node);
@@ -1202,7 +1217,9 @@ __device__ __forceinline__ bool oct_leaf(const OctDev &sc, uint32_t node, f3 bmi
   // through 8 v_mov per step.
   bool hit = false;
   float tp = t;
-  if (inside(p)) {
+  // FAST: p is the med3 clamp of a finite point into the box, which the
+  // in-box test (the same med3, compared) always passes
+  if (FAST || inside(p)) {
     bool in;
     do {
       const float s = oct_sdf(c, bmin, inv_s, p);
@@ -1312,7 +1329,7 @@ __device__ __forceinline__ void oct_filter(uint32_t &list, uint32_t &cnt, uint32
 // take the exact slab + sort8 path.
 template <bool FAST>
 __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float tNear, float tFar,
-                                           uint32_t keep, uint32_t &list, uint32_t &cnt) {
+                                           float P, float Q, uint32_t keep, uint32_t &list, uint32_t &cnt) {
   const f3 center{(bmin.x + bmax.x) / 2.0f, (bmin.y + bmax.y) / 2.0f, (bmin.z + bmax.z) / 2.0f};
   // divide_box_8's upper child max, center + (center - boxMin), IS bmax: every
   // value on the chain is an exact dyadic (oct_box), so the add is exact; the
@@ -1324,10 +1341,10 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
   const float z0 = (bmin.z - o.z) * inv.z, z1 = (center.z - o.z) * inv.z, z2 = (hi.z - o.z) * inv.z;
   bool exact = !FAST || !RT_OCT_PATH;
   if constexpr (FAST && RT_OCT_PATH) {
-    // near half per axis: 0 when the ray runs towards +axis (1/d > 0), else 1
+    // near half per axis: 0 when the ray runs towards +axis (1/d > 0), else 1.
+    // P = max(the 3 entries, tNear), Q = min(the 3 exits, tFar): oct_entry's
+    // t1 / t2 (an entry is the smaller of an axis' two slab distances)
     const bool px = inv.x > 0.0f, py = inv.y > 0.0f, pz = inv.z > 0.0f;
-    const float P = __builtin_fmaxf(__builtin_fmaxf(px ? x0 : x2, __builtin_fmaxf(py ? y0 : y2, pz ? z0 : z2)), tNear);
-    const float Q = __builtin_fminf(__builtin_fminf(px ? x2 : x0, __builtin_fminf(py ? y2 : y0, pz ? z2 : z0)), tFar);
     // the centre-plane distances in ascending order, with their child-id bits
     float s0 = x1, s1 = y1, s2 = z1;
     uint32_t b0 = 4u, b1 = 2u, b2 = 1u;
@@ -1345,11 +1362,10 @@ __device__ __forceinline__ void oct_expand(f3 bmin, f3 bmax, f3 o, f3 inv, float
     const float k0 = P, k1 = vmax_f32(P, s0), k2 = vmax_f32(P, s1), k3 = vmax_f32(P, s2);
     const float m0 = vmin_f32(Q, s0), m1 = vmin_f32(Q, s1), m2 = vmin_f32(Q, s2), m3 = Q;
     // entered and kept: the reference's !(tMax < 0 || tMin > tMax) && t > 0;
-    // with no NaN, k > 0 and k <= m imply m >= 0, so two compares suffice
-    // (written so the compiler does not fold them into an fmax that needs
-    // canonicalised operands)
-    const bool e0 = (k0 > 0.0f) & (m0 >= k0), e1 = (k1 > 0.0f) & (m1 >= k1);
-    const bool e2 = (k2 > 0.0f) & (m2 >= k2), e3 = (k3 > 0.0f) & (m3 >= k3);
+    // with no NaN, k > 0 and k <= m imply m >= 0, and k >= P >= tNear > 0
+    // (FAST rays have tNear > 0, oct_trace), so k <= m is the whole test
+    const bool e0 = m0 >= k0, e1 = m1 >= k1;
+    const bool e2 = m2 >= k2, e3 = m3 >= k3;
     // Ties among the kept entries: with s0 < s1 < s2, k_i = max(P, s_{i-1}) is
     // non-decreasing and k_i == k_{i+1} only when both are P, i.e. s_i <= P;
     // entry i also needs m_i = min(Q, s_i) >= k_i = P, so a tie of two kept
@@ -1476,10 +1492,11 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   if (root == 0 || root == rtl::kOctNeverHits) {
     cnt.add(C_OCT_LEAF, 1);
     if (root == rtl::kOctNeverHits) return RAY_MISS;
-    float lt;
+    float lt, P, Q;
     f3 lp;
-    if (!oct_leaf<FAST>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar, lt,
-                        lp, cnt))
+    oct_entry<FAST>(f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, o, inv, tNear, tFar, P, Q);
+    if (!oct_leaf<FAST>(sc, 0, f3{-1.0f, -1.0f, -1.0f}, f3{1.0f, 1.0f, 1.0f}, 0.5f, o, d, inv, tNear, tFar, P, Q,
+                        lt, lp, cnt))
       return RAY_MISS;
     out_t = lt;
     hp.p = lp;
@@ -1490,7 +1507,9 @@ __device__ __forceinline__ int oct_start(const OctDev &sc, f3 o, f3 d, f3 inv, f
   float inv_s;
   oct_box(0, 0, 0, 0, bmin, bmax, inv_s);
   uint32_t l, c;
-  oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, CT::kCounts ? 0xFFu : (rw.masks & 0xFFu), l, c);
+  float P, Q;
+  oct_entry<FAST>(bmin, bmax, o, inv, tNear, tFar, P, Q);
+  oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, P, Q, CT::kCounts ? 0xFFu : (rw.masks & 0xFFu), l, c);
   R = OctRay{root, l | (c << 24), rw.masks >> 8, 0u, 0u, 0u, 0, 0};
   return c == 0 ? RAY_MISS : RAY_PENDING;
 }
@@ -1562,11 +1581,15 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
     f3 bmin, bmax;
     float inv_s;
     oct_box(cxyz.ix(), cxyz.iy(), cxyz.iz(), depth + 1, bmin, bmax, inv_s);
+    // the box entry / exit, shared by the leaf and the inner-node paths (a
+    // wave whose lanes take both computes it once)
+    float P, Q;
+    oct_entry<FAST>(bmin, bmax, o, inv, tNear, tFar, P, Q);
     if (leaf) {
       cnt.add(C_OCT_LEAF, 1);
       float lt;
       f3 lp;
-      if (oct_leaf<FAST>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, lt, lp, cnt)) {
+      if (oct_leaf<FAST>(sc, cn, bmin, bmax, inv_s, o, d, inv, tNear, tFar, P, Q, lt, lp, cnt)) {
         out_t = lt;
         hp.p = lp;
         hp.node = cn; hp.ix = cxyz.ix(); hp.iy = cxyz.iy(); hp.iz = cxyz.iz(); hp.depth = depth + 1;
@@ -1575,7 +1598,7 @@ __device__ __forceinline__ int oct_run(const OctDev &sc, f3 o, f3 d, f3 inv, flo
       continue;
     }
     uint32_t l, c;
-    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, MASKS ? (cw.masks & 0xFFu) : 0xFFu, l, c);
+    oct_expand<FAST>(bmin, bmax, o, inv, tNear, tFar, P, Q, MASKS ? (cw.masks & 0xFFu) : 0xFFu, l, c);
     if (c == 0) continue;
     if (fcnt != 0) {
       st.at(sp, 0) = fbase;
@@ -1609,7 +1632,9 @@ __device__ __forceinline__ bool oct_trace(const OctDev &sc, f3 o, f3 d, float tN
                                           LdsStack<BLOCK, kOctFields> st, float &out_t, f3 &out_n,
                                           uint32_t &out_node, CT &cnt) {
   const f3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z))
+  // FAST: every 1/d finite and tNear > 0 (the render paths' 0.01;
+  // rt_intersect_rays callers may pass any tNear)
+  if (__builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z) && tNear > 0.0f)
     return oct_trace_t<BLOCK, NEED_NORMAL, true, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
   return oct_trace_t<BLOCK, NEED_NORMAL, false, PACK>(sc, o, d, inv, tNear, tFar, st, out_t, out_n, out_node, cnt);
 }
