@@ -810,6 +810,9 @@ __device__ __forceinline__ bool mesh_occluded(const MeshDev &sc, f3 o, f3 d, flo
 #ifndef RT_GRID_MUL24
 #define RT_GRID_MUL24 1  // A/B switch: 0 keeps 32-bit multiplies in the tap addressing
 #endif
+#ifndef RT_GRID_MARCH
+#define RT_GRID_MARCH 1  // A/B switch: 1 the march as a one-exit loop (grid_march), 0 the two-exit form
+#endif
 constexpr uint32_t kBrick = 4;
 constexpr uint64_t kGridLinearMaxBytes = 4ull << 20;
 struct GridDev {
@@ -976,6 +979,41 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
   p = vstd_max(p, f3{-1.0f, -1.0f, -1.0f});
   p = vstd_min(p, f3{1.0f, 1.0f, 1.0f});
   GridTaps tc;
+#if RT_GRID_MARCH
+  // One exit per step, as the octree's leaf march (oct_leaf): t advances by s
+  // on every step (the reference returns t + s at a hit), the next point and
+  // its in-box test are computed on the hit step too, and the hit point is
+  // rebuilt after the loop from the t it was computed at, clamped as above
+  // (the first step's point exactly; a later one passed the in-box test, so
+  // the clamp leaves it -- at most a zero's sign, which grid_normal's p +- E
+  // and the sdf's (p + 1) / 2 never see). The hit cell is the last step's c0
+  // sample, read from the tap cache's key after the loop.
+  // in the box: med3(q, -1, 1) == q on every axis (false for a NaN coordinate)
+  auto inside = [](f3 q) {
+    return clamp_med3(q.x, -1.0f, 1.0f) == q.x && clamp_med3(q.y, -1.0f, 1.0f) == q.y &&
+           clamp_med3(q.z, -1.0f, 1.0f) == q.z;
+  };
+  constexpr bool kCache = RT_GRID_TAP_CACHE != 0;
+  bool hit = false;
+  float tp = t;
+  if (inside(p)) {
+    bool in;
+    do {
+      const float s = grid_sdf_t<kMode, kCache>(g, p, kCache ? nullptr : &cell, tc, cnt);
+      hit = s < 1e-3f;
+      tp = t;
+      t += s;
+      p = o + t * d;
+      in = inside(p);
+    } while (!hit && in);
+  }
+  if (hit) {
+    out_t = t;
+    hp = vstd_min(vstd_max(o + tp * d, f3{-1.0f, -1.0f, -1.0f}), f3{1.0f, 1.0f, 1.0f});
+    if (kCache) cell = (tc.i0x * g.sy + tc.i0y) * g.sz + tc.i0z;
+  }
+  return hit;
+#else
   while (p.x <= 1.0f && p.y <= 1.0f && p.z <= 1.0f && p.x >= -1.0f && p.y >= -1.0f && p.z >= -1.0f) {
     const float s = grid_sdf_t<kMode, RT_GRID_TAP_CACHE != 0>(g, p, &cell, tc, cnt);
     if (s < 1e-3f) {
@@ -987,6 +1025,7 @@ __device__ __forceinline__ bool grid_march(const GridDev &g, f3 o, f3 d, float t
     p = o + t * d;
   }
   return false;
+#endif
 }
 
 template <int kMode, class CT>
