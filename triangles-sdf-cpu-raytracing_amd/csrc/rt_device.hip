@@ -579,6 +579,13 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 // centre-out order that dispatches the model tiles first (octree 4K primary
 // 1.15 -> 1.29 ms: the heavy tiles then compete for the same CUs at once).
 
+// Diagnostic switch (never in a shipping build): 1 drops the stores into host
+// frames, 2 keeps only their colour stores, to time what the traversal costs
+// without them
+#ifndef RT_DIAG_HOST_NOSTORE
+#define RT_DIAG_HOST_NOSTORE 0
+#endif
+
 // One pixel per lane of the wave's 8x8 tile: column xo, rank-local row yl.
 // Returns true iff this lane stored a hit (its pixel differs from a cleared
 // frame's or from tPrev).
@@ -631,7 +638,11 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     }
     // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
     const bool store = hit && !__builtin_isinf(t);
-    if (!active) {
+    if (RT_DIAG_HOST_NOSTORE == 1 && (fa.flags & kFlagHostFrame)) {
+      // diagnostic build only: a host frame's stores dropped (wrong output)
+    } else if (RT_DIAG_HOST_NOSTORE == 2 && (fa.flags & kFlagHostFrame)) {
+      if (active && store) fb_store(fa.color + idx, pack_rgba(c), sys);  // (colour only)
+    } else if (!active) {
       // helper lane of the cooperative path: no pixel of its own
     } else if (clear && !hits_only) {
       fb_store(fa.color + idx, store ? pack_rgba(c) : 0u, sys);
@@ -3083,6 +3094,9 @@ int rtx_render_inject_failure(int32_t n) {
 }
 int64_t rtx_render_drain_count(void) { return g_render_drains.load(); }
 
+#ifndef RT_PIN_COARSE
+#define RT_PIN_COARSE 1  // A/B switch: 0 registers caller ranges fine-grained (the HIP default)
+#endif
 int rt_host_pin(void *ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return set_err(RT_E_INVALID, "bad host range");
   {
@@ -3092,8 +3106,22 @@ int rt_host_pin(void *ptr, int64_t bytes) {
       return set_err(RT_E_INVALID, "rt_host_pin: the range overlaps a range pinned earlier and not unpinned "
                                    "(a buffer freed without rt_host_unpin?)");
   }
-  // portable: mapped on every device (rt_multi_render's slots store into it)
-  const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+  // portable: mapped on every device (rt_multi_render's slots store into it).
+  // Coarse-grained (RT_PIN_COARSE): the range is coherent with the host at
+  // kernel and copy boundaries only -- which is all the library relies on: the
+  // host reads or writes a pinned frame only after the stream that used it is
+  // synchronised, and a dispatch's end-of-kernel release covers its stores --
+  // so the GPU's stores into it are not snooped by the host's caches: the
+  // zero-copy cleared frame's kernel (hits stored into the caller's pinned
+  // buffers) ran 0.19-0.24 ms into a fine-grained registration against
+  // ~0.18 into the library's own (coarse-grained) hipHostMalloc staging frame
+  // (profiles/r06/pin_coarse_ab.txt)
+  hipError_t e = hipHostRegister(ptr, (size_t)bytes,
+                                 hipHostRegisterMapped | hipHostRegisterPortable | (RT_PIN_COARSE ? hipExtHostRegisterCoarseGrained : 0u));
+  if (RT_PIN_COARSE && e == hipErrorInvalidValue) {  // (a runtime without the flag)
+    (void)hipGetLastError();
+    e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+  }
   if (e == hipErrorHostMemoryAlreadyRegistered) {
     (void)hipGetLastError();
     return set_err(RT_E_INVALID, "rt_host_pin: the HIP runtime already holds a registration over this range "
