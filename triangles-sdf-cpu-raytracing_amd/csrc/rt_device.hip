@@ -586,12 +586,33 @@ __device__ __forceinline__ void flush_counts(LaneCnt &c, unsigned long long *out
 #define RT_DIAG_HOST_NOSTORE 0
 #endif
 
+// Host-frame pair flush (one-frame kernel, 16x16 tiles of 4 waves). The
+// stores of a cleared frame in host memory (rt_render's and rt_multi_render's
+// zero-copy frames) cross the host link, where their number, not their bytes,
+// is what costs: an 8x8 wave tile's rows are 32-byte pieces, and the stores
+// were 45-95 us of the one-frame kernel's ~0.19 ms (dropping only the t
+// stores took ~3/4 of that, profiles/r06/dropin_host_store_cost.txt). The two
+// waves side by side in a tile (one 16-pixel row band of 8 rows) therefore
+// leave their pixels in LDS -- a miss as the cleared frame's words, which the
+// host frame already holds -- and the second of the two to finish writes the
+// band's 8 rows of colour and t as 64-byte pieces (one 16-byte store per
+// lane), or nothing when neither wave stored a hit. Taken for whole bands
+// inside the frame with 16-byte aligned rows (W % 4 == 0, aligned buffers);
+// other bands store per pixel as before. RT_PAIR_FLUSH=0: off (A/B switch).
+#ifndef RT_PAIR_FLUSH
+#define RT_PAIR_FLUSH 1
+#endif
+constexpr int kPairWords = 2 * 8 * 16;  // per buffer: 2 bands x 8 rows x 16 pixels
+
 // One pixel per lane of the wave's 8x8 tile: column xo, rank-local row yl.
 // Returns true iff this lane stored a hit (its pixel differs from a cleared
 // frame's or from tPrev).
+// defer (host-frame pair flush, render_body): this lane's colour and t words
+// go to defer[0] and defer[kPairWords] in LDS instead of the frame
 template <class S, int SLOTS, bool GENERAL, int DIAG, int B = kBlock, class CT>
 __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
-                                              CT &cnt, uint32_t *stk, int xo, int yl) {
+                                              CT &cnt, uint32_t *stk, int xo, int yl,
+                                              uint32_t *defer = nullptr) {
   const bool active = xo < fa.W && yl < fa.rows_local;
   // wave-cooperative primary path: every lane of the wave takes part
   constexpr bool kWaveCoop = DIAG == 0 && !GENERAL && S::kCoop;
@@ -638,7 +659,12 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
     }
     // the reference stores only when !isinf(tNew) (raytracing.cpp:91-94)
     const bool store = hit && !__builtin_isinf(t);
-    if (RT_DIAG_HOST_NOSTORE == 1 && (fa.flags & kFlagHostFrame)) {
+    if (defer) {
+      // a cleared host frame's pixel, hit or not: the pair flush writes whole
+      // rows (a miss's words are the cleared frame's own)
+      defer[0] = store ? pack_rgba(c) : 0u;
+      defer[kPairWords] = __float_as_uint(store ? t : kInf);
+    } else if (RT_DIAG_HOST_NOSTORE == 1 && (fa.flags & kFlagHostFrame)) {
       // diagnostic build only: a host frame's stores dropped (wrong output)
     } else if (RT_DIAG_HOST_NOSTORE == 2 && (fa.flags & kFlagHostFrame)) {
       if (active && store) fb_store(fa.color + idx, pack_rgba(c), sys);  // (colour only)
@@ -656,9 +682,20 @@ __device__ __forceinline__ bool render_pixels(const S &sc, const PlaneDev &pl, c
   return false;
 }
 
+// 16 bytes into a host frame, written through to memory at system scope (the
+// 16-byte form of fb_store's system-scope relaxed store: global_store ... sc0 sc1)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void host_store16(uint32_t *p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
+// hf: the pair-flush LDS (render_kernel; nullptr elsewhere): kPairWords colour
+// words, kPairWords t words, then one arrival counter per band (zeroed by the
+// kernel before any wave gets here)
 template <class S, int SLOTS, bool GENERAL, int DIAG, int BT = kBlock>
 __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, const FrameArgs &fa,
-                                            unsigned long long *counters, uint32_t *stk) {
+                                            unsigned long long *counters, uint32_t *stk,
+                                            uint32_t *hf = nullptr) {
   typename CntSel<DIAG>::T cnt{};
   unsigned long long t_start = 0;
   if (DIAG == 2) t_start = __builtin_amdgcn_s_memrealtime();
@@ -672,7 +709,36 @@ __device__ __forceinline__ void render_body(const S &sc, const PlaneDev &pl, con
   const uint64_t c0 = (DIAG == 0 && fa.cost) ? __builtin_amdgcn_s_memtime() : 0;
   const int xo = BT == 64 ? (int)bx * 8 + (lane & 7) : (int)bx * kTile + (wave & 1) * 8 + (lane & 7);
   const int yl = BT == 64 ? (int)by * 8 + (lane >> 3) : (int)by * kTile + (wave >> 1) * 8 + (lane >> 3);
-  const bool stored = render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, xo, yl);
+  // host-frame pair flush: this wave's band of 8 rows x 16 pixels lies inside
+  // the frame and its rows are 16-byte aligned (wave-uniform; the same for
+  // both waves of the band)
+  const int band = wave >> 1;
+  const bool flush = RT_PAIR_FLUSH && DIAG == 0 && BT == kBlock && hf != nullptr &&
+                     (fa.flags & kFlagHostFrame) && (fa.flags & RT_FLAG_CLEAR) && (fa.flags & RT_FLAG_HITS_ONLY) &&
+                     (fa.W & 3) == 0 && (((uintptr_t)fa.color | (uintptr_t)fa.t) & 15u) == 0 &&
+                     (int)bx * kTile + kTile <= fa.W && (int)by * kTile + band * 8 + 8 <= fa.rows_local;
+  uint32_t *slot = flush ? hf + band * 128 + (lane >> 3) * 16 + (wave & 1) * 8 + (lane & 7) : nullptr;
+  const bool stored = render_pixels<S, SLOTS, GENERAL, DIAG, BT>(sc, pl, fa, cnt, stk, xo, yl, slot);
+  if (flush) {
+    const uint32_t any = __ballot(stored) != 0 ? 1u : 0u;
+    // this wave's LDS words are written before its arrival is counted, and the
+    // band's second wave reads them only after counting its own
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t old = 0;
+    if (lane == 0) old = atomicAdd(hf + 2 * kPairWords + band, 1u | (any << 16));
+    old = __builtin_amdgcn_readfirstlane(old);
+    if ((old & 0xFFFFu) == 1u && (any | (old >> 16)) != 0u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      // lanes 0-31 write the colour rows, 32-63 the t rows: row r, 4 pixels at 4 ch
+      const int b = lane >> 5, r = (lane & 31) >> 2, ch = lane & 3;
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(hf + b * kPairWords + band * 128 + r * 16 + ch * 4);
+      const int ylr = (int)by * kTile + band * 8 + r;
+      const bool natural = (fa.flags & (kSysStoreFlags | kFlagNatural)) != 0;
+      const uint32_t row = (uint32_t)(natural ? image_row(ylr, fa) : ylr);
+      uint32_t *base = b ? reinterpret_cast<uint32_t *>(fa.t) : fa.color;
+      host_store16(base + row * (uint32_t)fa.W + (uint32_t)bx * kTile + (uint32_t)ch * 4u, v);
+    }
+  }
   if constexpr (DIAG == 0) {
     if (fa.hit_box && !(fa.flags & kFlagRowSpan) && __ballot(stored)) {  // this wave's stored pixels into the frame's hit box
       int32_t v[4] = {stored ? xo : INT32_MAX, stored ? -xo : INT32_MAX, stored ? yl : INT32_MAX,
@@ -791,12 +857,19 @@ __global__ __launch_bounds__(frame_block<DIAG>()) __attribute__((amdgpu_waves_pe
 void render_kernel(S sc_arg, PlaneDev pl, FrameArgs fa,
                                                         unsigned long long *counters) {
   __shared__ uint32_t stk[SLOTS * S::kFields * frame_block<DIAG>()];
+  constexpr bool kPair = RT_PAIR_FLUSH && DIAG == 0 && frame_block<DIAG>() == kBlock;
+  __shared__ __attribute__((aligned(16))) uint32_t hf[kPair ? 2 * kPairWords + 4 : 4];
   S sc = sc_arg;
   if constexpr (S::kCoop && !GENERAL && DIAG == 0) {
     sc.prio_iters = RT_FRAME_PRIO;
     sc.coop_rays = RT_FRAME_COOP;
   }
-  render_body<S, SLOTS, GENERAL, DIAG, frame_block<DIAG>()>(sc, pl, fa, counters, stk);
+  // (grid-uniform condition: every wave of the block passes the barrier or none)
+  if (kPair && (fa.flags & kFlagHostFrame) && (fa.flags & RT_FLAG_CLEAR) && (fa.flags & RT_FLAG_HITS_ONLY)) {
+    if (threadIdx.x < 2) hf[2 * kPairWords + threadIdx.x] = 0u;
+    __syncthreads();
+  }
+  render_body<S, SLOTS, GENERAL, DIAG, frame_block<DIAG>()>(sc, pl, fa, counters, stk, kPair ? hf : nullptr);
   peer_release(fa.flags);
 }
 
