@@ -185,7 +185,11 @@ int rt_render(rt_scene *s, const rt_render_params *p, uint32_t *color, float *t,
  * that overlaps one still pinned). rt_host_unpin first drains every stream the
  * library created. Optional: on pageable memory the library copies through its
  * own pinned staging frames on the host, so the HIP runtime never DMAs from or
- * to a caller's pageable memory. */
+ * to a caller's pageable memory. The range is
+ * registered coarse-grained: it is coherent with the host at stream
+ * synchronisation points only, which every rt_render / rt_multi_render call
+ * reaches before it returns; a caller that hands the same range to its own
+ * HIP work must synchronise that work before reading the range on the host. */
 int rt_host_pin(void *ptr, int64_t bytes);
 int rt_host_unpin(void *ptr);
 /* Same on DEVICE buffers, asynchronously on `stream` (hipStream_t or NULL).
