@@ -346,6 +346,53 @@ def test_drop_in_cleared_frames_zero_copy(gpu, pinned):
                 L.rt_host_unpin(t.ctypes.data)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_drop_in_cleared_pair_flush_layouts(gpu, pinned):
+    """The one-frame kernel writes a cleared host frame's 16-pixel bands as
+    64-byte row pieces from LDS (the pair flush) only for bands inside the
+    frame with 16-byte aligned rows; every other band stores per pixel. Frames
+    whose buffers start 0, 4, 8 and 12 bytes past an aligned address, widths
+    that are and are not multiples of 4, and heights that end inside a band
+    all equal the device-frame path bitwise (and the oracle's frame for the
+    aligned case)."""
+    rt = gpu
+    L = rt.lib()
+    name = "stanford-bunny.obj"
+    sc = S.gpu_scene(name)
+    S.set_planes(name, "default", sc)
+    rs = S.ref_scene(name)
+    S.set_planes(name, "default", rs)
+    pos = (0.1, 0.2, 2.2)
+    for W, H in ((320, 180), (322, 181), (336, 96)):
+        P = S.params(name, W, H, "default", pos, "gpu")
+        rc = np.zeros((H, W), np.uint32)
+        rt_ = np.full((H, W), np.inf, np.float32)
+        sc.render(P, rc, rt_, clear=True)
+        if (W, H) == (320, 180):
+            oc, ot, _, _ = rs.render(S.params(name, W, H, "default", pos, "ref"), W, H)
+            assert np.array_equal(rc, oc) and np.array_equal(rt_.view(np.uint32), ot.view(np.uint32))
+        for off in (0, 1, 2, 3):  # words past a 64-byte aligned base
+            rawc = np.zeros(H * W + 32, np.uint32)
+            rawt = np.zeros(H * W + 32, np.float32)
+            bc = (-(rawc.ctypes.data // 4)) % 16 + off
+            bt = (-(rawt.ctypes.data // 4)) % 16 + off
+            c = rawc[bc:bc + H * W].reshape(H, W)
+            t = rawt[bt:bt + H * W].reshape(H, W)
+            c[:] = 0
+            t[:] = np.inf
+            if pinned:
+                rt._lib.check(L.rt_host_pin(c.ctypes.data, c.nbytes))
+                rt._lib.check(L.rt_host_pin(t.ctypes.data, t.nbytes))
+            try:
+                sc.render(P, c, t, cleared=True)
+            finally:
+                if pinned:
+                    L.rt_host_unpin(c.ctypes.data)
+                    L.rt_host_unpin(t.ctypes.data)
+            assert np.array_equal(c, rc), (W, H, off, int((c != rc).sum()))
+            assert np.array_equal(t.view(np.uint32), rt_.view(np.uint32)), (W, H, off)
+
+
 def test_hits_only_needs_clear(gpu):
     from rtamd import _lib
     sc = S.gpu_scene("cube.obj")
