@@ -1,3 +1,8 @@
+# Round-6 re-sweep of the mesh tail parameters in the driver's shape (headline
+# only, 20 steps), three interleaved rounds (profiles/r06/param_sweep_majority.txt).
+# Build the variants first:
+#   bash tools/build_variant.sh coop12 -DRT_COOP_RAYS=12; ... coop16 -DRT_COOP_RAYS=16;
+#   prio8 -DRT_HEAVY_PRIO=8; prio32 -DRT_HEAVY_PRIO=32; prio0 -DRT_HEAVY_PRIO=0
 L=$PWD/triangles-sdf-cpu-raytracing_amd/lib
 mkdir -p gpurun_out/sweep
 for r in 1 2 3; do
