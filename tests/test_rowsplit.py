@@ -346,8 +346,9 @@ def test_drop_in_cleared_frames_zero_copy(gpu, pinned):
                 L.rt_host_unpin(t.ctypes.data)
 
 
+@pytest.mark.parametrize("name", ["stanford-bunny.obj", "example_grid.grid", "sdf_6.octree"])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_drop_in_cleared_pair_flush_layouts(gpu, pinned):
+def test_drop_in_cleared_pair_flush_layouts(gpu, pinned, name):
     """The one-frame kernel writes a cleared host frame's 16-pixel bands as
     64-byte row pieces from LDS (the pair flush) only for bands inside the
     frame with 16-byte aligned rows; every other band stores per pixel. Frames
@@ -357,13 +358,13 @@ def test_drop_in_cleared_pair_flush_layouts(gpu, pinned):
     aligned case)."""
     rt = gpu
     L = rt.lib()
-    name = "stanford-bunny.obj"
     sc = S.gpu_scene(name)
     S.set_planes(name, "default", sc)
     rs = S.ref_scene(name)
     S.set_planes(name, "default", rs)
     pos = (0.1, 0.2, 2.2)
-    for W, H in ((320, 180), (322, 181), (336, 96)):
+    sizes = ((320, 180), (322, 181), (336, 96)) if name.endswith(".obj") else ((320, 180), (322, 181))
+    for W, H in sizes:
         P = S.params(name, W, H, "default", pos, "gpu")
         rc = np.zeros((H, W), np.uint32)
         rt_ = np.full((H, W), np.inf, np.float32)
