@@ -1787,6 +1787,9 @@ int ensure_stage(rt_scene *s, size_t px) {
 // order kernel runs on the side stream after it, concurrently with the next
 // frame -- so back-to-back one-frame launches never queue behind an order
 // kernel (~8 us at 1080p), at the price of an order two frames old.
+#ifndef RT_SCHED_FRESH
+#define RT_SCHED_FRESH 1  // A/B switch: 0 always renders in the order two frames old
+#endif
 int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStream_t stream) {
   fa.order = nullptr;
   fa.cost = nullptr;
@@ -1832,7 +1835,18 @@ int schedule_begin(rt_scene *s, FrameArgs &fa, uint32_t gx, uint32_t gy, hipStre
       HIP_TRY(q);
     }
   }
-  if (s->sched_key[p] == ((gx << 16) | gy)) fa.order = s->d_order[p];
+  const uint32_t key = (gx << 16) | gy;
+  // The previous frame's order when its order kernel has already finished --
+  // a frame issued after the host waited for the one before it (the drop-in's
+  // Renderer::draw loop) -- else the one two frames old. The previous frame's
+  // order buffer is rewritten only by the next frame's order kernel, which
+  // runs after the next frame, so after this one.
+  if (RT_SCHED_FRESH && s->ord_rec[p ^ 1] && s->sched_key[p ^ 1] == key &&
+      hipEventQuery(s->ord_ev[p ^ 1]) == hipSuccess) {
+    fa.order = s->d_order[p ^ 1];
+  } else if (s->sched_key[p] == key) {
+    fa.order = s->d_order[p];
+  }
   fa.cost = s->d_cost[p];
   return RT_OK;
 }
